@@ -1,0 +1,171 @@
+"""bench.py — Siamese fwd+bwd graph-pairs/s on AIDS700nef-shaped all-pairs.
+
+One step = one pass of the hot path over the whole 700² = 490,000-pair
+all-pairs batch: fused forward + broadcast-MSE loss + backward over this rank's
+pair shard, deterministic gradient reduction, RCCL all-reduce of the flat
+gradient (N > 1), TF-form Adam.  Inputs (packed pair records) are resident in
+HBM before timing starts.  Prints ONE JSON line (rank 0).
+
+  python bench.py [--gpus N --steps K --warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3       # gfx950 fp32 peak (vector = f32 MFMA), MI355X_MICROARCH.md
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=20)
+    p.add_argument('--warmup', type=int, default=3)
+    p.add_argument('--dataset', default='syn_aids700nef')
+    p.add_argument('--dropout', type=float, default=0.1)
+    p.add_argument('--cpu-sample', type=int, default=0,
+                   help='pairs for the CPU baseline (0 = auto, -1 = skip)')
+    p.add_argument('--json-out', default='')
+    return p.parse_args()
+
+
+def cpu_baseline(gs, labels, flags, n_sample):
+    """Time the oracle's C restatement (oracle/siamese_cpu.c, OpenMP) on a
+    bounded sample of the same all-pairs stream, on this host's cores."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    from oracle import cpu_ref
+    return cpu_ref.time_allpairs_sample(gs, labels, flags, n_sample)
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    device = torch.device('cuda', local)
+
+    from graphembedding_amd.allpairs import AllPairsShard, load_graph_set
+    from graphembedding_amd.config import Flags
+    from graphembedding_amd.model_mse import SiameseGCNTNMSE
+    from graphembedding_amd.shard import make_allreduce_hook
+
+    flags = Flags(dropout=args.dropout)
+    gs = load_graph_set(args.dataset, n_max=10)
+    labels = gs.label_matrix(flags.yeta)
+    model = SiameseGCNTNMSE(gs.d_in, flags, device=device, n_max=gs.n_max)
+    shard = AllPairsShard(gs, labels, rank, world, device=device)
+    batch = shard.batch(model)
+    hook = make_allreduce_hook() if world > 1 else None
+    model.workspace(batch.n_pairs)
+    stream = torch.cuda.current_stream()
+
+    ev = []
+
+    def step(timed):
+        if timed:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        model.fwd_bwd(batch, add_label_term=(rank == 0))
+        if timed:
+            e1.record(stream)
+            ev.append((e0, e1))
+        if hook is not None:
+            hook(model)
+        model.apply_adam()
+        model.step_count += 1
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    total_pairs = shard.total
+    value = total_pairs * args.steps / elapsed
+    loss = float(model.loss_buf[0].item() + model.reg_buf[0].item())
+
+    if rank == 0:
+        flops_pair = gs.flops_per_pair()
+        bytes_pair = shard.record_bytes
+        kern_pairs_s = shard.n / (kern_ms * 1e-3)
+        achieved_tf = kern_pairs_s * flops_pair / 1e12
+        achieved_gbs = kern_pairs_s * bytes_pair / 1e9
+        cpu = None
+        if world == 1 and args.cpu_sample >= 0:
+            try:
+                cpu = cpu_baseline(gs, labels, flags, args.cpu_sample)
+            except Exception as e:  # reported, never fatal for the GPU number
+                cpu = {'value': None, 'unit': 'graph-pairs/s', 'cores': 0, 'kind': 'port',
+                       'sample': 'failed: {}'.format(e)}
+        out = {
+            'metric': 'graph-pairs/sec (Siamese fwd+bwd), AIDS700 all-pairs',
+            'value': value,
+            'unit': 'graph-pairs/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': elapsed * 1e3 / args.steps,
+            'higher_is_better': True,
+            'scaling': 'strong',
+            'vs_baseline': None,
+            'dtype': 'f32',
+            'data': 'synthetic (AIDS700nef-shaped graphs + GED labels, BASELINE.md §3)',
+            'config': {'workload': 'AIDS700nef all-pairs (700 graphs, 490,000 ordered pairs), '
+                                   'default 5-layer Siamese GCN-NTN, dropout {}'.format(args.dropout),
+                       'global_batch': total_pairs, 'n_max': gs.n_max, 'd_in': gs.d_in,
+                       'kernel_path': 'fused' if model.kernel_path == 1 else 'generic',
+                       'parallelism': 'dp{}'.format(world)},
+            'roofline': {'bound': 'mfma', 'achieved': achieved_tf, 'peak': FP32_PEAK_TFLOPS,
+                         'unit': 'TFLOP/s', 'frac': achieved_tf / FP32_PEAK_TFLOPS,
+                         'traffic': None,
+                         'note': 'fp32 compute roof (gfx950 vector fp32 == f32 MFMA peak); '
+                                 'algorithmic {:.0f} FLOP/pair x {} pairs per launch / sg_fwd_bwd '
+                                 'event time {:.3f} ms'.format(flops_pair, shard.n, kern_ms)},
+            'roofline_hbm': {'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                             'frac': achieved_gbs / HBM_PEAK_GBS,
+                             'bytes_per_pair': bytes_pair},
+            'cpu_baseline': cpu,
+            'loss': loss,
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, 'w') as f:
+                f.write(line + '\n')
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

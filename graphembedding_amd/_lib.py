@@ -1,0 +1,213 @@
+"""ctypes binding of libsiamese_hip.so (C-ABI declared in include/siamese_hip.h).
+
+The product path has no CPU fallback: if the HIP library is missing or cannot
+be loaded this module raises, loudly, on first use.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'lib', 'libsiamese_hip.so')
+
+SG_OK, SG_ERR_ARG, SG_ERR_UNSUPPORTED, SG_ERR_HIP, SG_ERR_SHAPE = 0, 1, 2, 3, 4
+_ERR_NAMES = {1: 'SG_ERR_ARG', 2: 'SG_ERR_UNSUPPORTED', 3: 'SG_ERR_HIP', 4: 'SG_ERR_SHAPE'}
+
+SG_GCN, SG_DENSE, SG_PADDING, SG_AVERAGE, SG_ATTENTION, SG_NTN, SG_DOT = 1, 2, 3, 4, 5, 6, 7
+KIND_CODES = {'GraphConvolution': SG_GCN, 'Dense': SG_DENSE, 'Padding': SG_PADDING,
+              'Average': SG_AVERAGE, 'Attention': SG_ATTENTION, 'NTN': SG_NTN, 'Dot': SG_DOT}
+ACT_CODES = {'identity': 0, 'relu': 1, 'sigmoid': 2, 'tanh': 3}
+FINAL_GAUSSIAN, FINAL_IDENTITY, FINAL_RELU, FINAL_SIGMOID, FINAL_TANH = 0, 1, 2, 3, 4
+LOSS_BROADCAST, LOSS_ALIGNED = 0, 1
+NTN_REFERENCE, NTN_INTENDED = 0, 1
+SG_MAX_LAYERS = 8
+
+
+class SgLayer(ctypes.Structure):
+    _fields_ = [('kind', ctypes.c_int32), ('input_dim', ctypes.c_int32),
+                ('output_dim', ctypes.c_int32), ('act', ctypes.c_int32),
+                ('bias', ctypes.c_int32), ('dropout', ctypes.c_int32),
+                ('sparse_inputs', ctypes.c_int32), ('padding_value', ctypes.c_float)]
+
+
+class SgModel(ctypes.Structure):
+    _fields_ = [('num_layers', ctypes.c_int32), ('d_in', ctypes.c_int32),
+                ('n_max', ctypes.c_int32), ('final_act', ctypes.c_int32),
+                ('loss_mode', ctypes.c_int32), ('ntn_mode', ctypes.c_int32),
+                ('keep_prob', ctypes.c_float), ('yeta', ctypes.c_float),
+                ('layers', SgLayer * SG_MAX_LAYERS)]
+
+
+class SiameseHipError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load the HIP library (raises SiameseHipError if it is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.isfile(LIB_PATH):
+        raise SiameseHipError(
+            'libsiamese_hip.so not found at {} — run `python -c "import __graft_entry__ as g; '
+            'g.build()"` (hipcc --offload-arch=gfx950). There is no CPU fallback.'.format(LIB_PATH))
+    L = ctypes.CDLL(LIB_PATH)
+    c_i32, c_i64, c_u64, c_f = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float
+    vp = ctypes.c_void_p
+    pm = ctypes.POINTER(SgModel)
+    L.sg_version.restype = c_i32
+    L.sg_record_bytes.argtypes = [c_i32]
+    L.sg_record_bytes.restype = c_i64
+    L.sg_model_validate.argtypes = [pm, ctypes.POINTER(c_i64), ctypes.POINTER(c_i32)]
+    L.sg_model_validate.restype = c_i32
+    L.sg_workspace_bytes.argtypes = [pm, c_i64]
+    L.sg_workspace_bytes.restype = c_i64
+    L.sg_pack_pairs.argtypes = [vp, vp, vp, c_i32, c_i32, vp, vp, c_i64, vp, vp, vp]
+    L.sg_pack_pairs.restype = c_i32
+    L.sg_label_stats.argtypes = [vp, c_i64, c_i32, vp, vp, vp]
+    L.sg_label_stats.restype = c_i32
+    L.sg_forward.argtypes = [pm, vp, c_i64, c_i64, vp, c_u64, vp, vp, vp]
+    L.sg_forward.restype = c_i32
+    L.sg_fwd_bwd.argtypes = [pm, vp, c_i64, c_i64, c_i64, vp, c_u64, vp, c_i32, vp, vp, vp, vp, vp]
+    L.sg_fwd_bwd.restype = c_i32
+    L.sg_adam_tf.argtypes = [vp, vp, vp, vp, c_i64, c_f, c_f, c_f, c_f, c_f, vp, vp, vp]
+    L.sg_adam_tf.restype = c_i32
+    _lib = L
+    return L
+
+
+EXPORTED_SYMBOLS = ('sg_version', 'sg_record_bytes', 'sg_model_validate', 'sg_workspace_bytes',
+                    'sg_pack_pairs', 'sg_label_stats', 'sg_forward', 'sg_fwd_bwd', 'sg_adam_tf')
+
+
+def check(rc: int, what: str) -> None:
+    if rc != SG_OK:
+        raise SiameseHipError('{} failed: {} ({})'.format(what, _ERR_NAMES.get(rc, rc), rc))
+
+
+def final_act_code(final_act: str, sim_kernel: str) -> int:
+    if final_act == 'sim_kernel':
+        if sim_kernel == 'gaussian':
+            return FINAL_GAUSSIAN
+        if sim_kernel == 'identity':
+            return FINAL_IDENTITY
+        raise RuntimeError('Unknown sim kernel {}'.format(sim_kernel))
+    codes = {'identity': FINAL_IDENTITY, 'relu': FINAL_RELU, 'sigmoid': FINAL_SIGMOID,
+             'tanh': FINAL_TANH}
+    if final_act not in codes:
+        raise RuntimeError('Unknown activation function {}'.format(final_act))
+    return codes[final_act]
+
+
+def make_model(layers: List[dict], d_in: int, n_max: int, keep_prob: float, final_act: str,
+               sim_kernel: str, yeta: float, loss_mode: str = 'broadcast',
+               ntn_mode: str = 'reference') -> SgModel:
+    """Layer dicts (graphembedding_amd.layers_factory format) → sg_model_t."""
+    if len(layers) > SG_MAX_LAYERS:
+        raise RuntimeError('at most {} layers supported'.format(SG_MAX_LAYERS))
+    m = SgModel()
+    m.num_layers = len(layers)
+    m.d_in = int(d_in)
+    m.n_max = int(n_max)
+    m.final_act = final_act_code(final_act, sim_kernel)
+    m.loss_mode = {'broadcast': LOSS_BROADCAST, 'aligned': LOSS_ALIGNED}[loss_mode]
+    m.ntn_mode = {'reference': NTN_REFERENCE, 'intended': NTN_INTENDED}[ntn_mode]
+    m.keep_prob = float(keep_prob)
+    m.yeta = float(yeta if yeta is not None else 0.0)
+    for i, L in enumerate(layers):
+        s = m.layers[i]
+        s.kind = KIND_CODES[L['kind']]
+        k = L['kind']
+        if k == 'GraphConvolution':
+            s.input_dim = int(L.get('input_dim') or 0)
+            s.output_dim = int(L['output_dim'])
+            s.act = ACT_CODES[L['act']]
+            s.sparse_inputs = int(bool(L['sparse_inputs']))
+        elif k == 'Dense':
+            s.input_dim = int(L['input_dim'])
+            s.output_dim = int(L['output_dim'])
+            s.act = ACT_CODES[L['act']]
+        elif k == 'Padding':
+            s.output_dim = int(L['max_in_dims'])
+            s.padding_value = float(L.get('padding_value', 0))
+        elif k == 'Attention':
+            s.input_dim = int(L['input_dim'])
+        elif k == 'NTN':
+            s.input_dim = int(L['input_dim'])
+            s.output_dim = int(L['feature_map_dim'])
+            s.act = ACT_CODES[L['inneract']]
+        s.bias = int(bool(L.get('bias', False)))
+        s.dropout = int(bool(L.get('dropout', False)))
+    return m
+
+
+def validate(m: SgModel):
+    """Returns (n_params, path) where path 1 = fused fast kernel, 0 = generic."""
+    n = ctypes.c_int64(0)
+    p = ctypes.c_int32(0)
+    check(lib().sg_model_validate(ctypes.byref(m), ctypes.byref(n), ctypes.byref(p)),
+          'sg_model_validate')
+    return int(n.value), int(p.value)
+
+
+def record_bytes(n_max: int) -> int:
+    return int(lib().sg_record_bytes(int(n_max)))
+
+
+def _ptr(t) -> Optional[int]:
+    return None if t is None else int(t.data_ptr())
+
+
+def _stream(stream) -> Optional[int]:
+    if stream is None:
+        import torch
+        return int(torch.cuda.current_stream().cuda_stream)
+    return int(stream)
+
+
+def workspace_bytes(m: SgModel, n_pairs: int) -> int:
+    b = int(lib().sg_workspace_bytes(ctypes.byref(m), int(n_pairs)))
+    if b < 0:
+        raise SiameseHipError('sg_workspace_bytes: unsupported model')
+    return b
+
+
+def pack_pairs(store_adj, store_types, store_n, n_max, pair_idx, labels, records, status=None,
+               stream=None):
+    n_graphs = int(store_n.shape[0])
+    n_pairs = int(pair_idx.shape[0])
+    check(lib().sg_pack_pairs(_ptr(store_adj), _ptr(store_types), _ptr(store_n), n_graphs,
+                              int(n_max), _ptr(pair_idx), _ptr(labels), n_pairs, _ptr(records),
+                              _ptr(status), _stream(stream)), 'sg_pack_pairs')
+
+
+def label_stats(records, n_pairs, n_max, stats_out, workspace, stream=None):
+    check(lib().sg_label_stats(_ptr(records), int(n_pairs), int(n_max), _ptr(stats_out),
+                               _ptr(workspace), _stream(stream)), 'sg_label_stats')
+
+
+def forward(m: SgModel, records, n_pairs, pair_offset, params, seed, s_out, workspace=None,
+            stream=None):
+    check(lib().sg_forward(ctypes.byref(m), _ptr(records), int(n_pairs), int(pair_offset),
+                           _ptr(params), int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(s_out),
+                           _ptr(workspace), _stream(stream)), 'sg_forward')
+
+
+def fwd_bwd(m: SgModel, records, n_pairs, pair_offset, batch_total, params, seed, y_stats,
+            add_label_term, s_out, grad_out, loss_out, workspace, stream=None):
+    check(lib().sg_fwd_bwd(ctypes.byref(m), _ptr(records), int(n_pairs), int(pair_offset),
+                           int(batch_total), _ptr(params), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                           _ptr(y_stats), int(add_label_term), _ptr(s_out), _ptr(grad_out),
+                           _ptr(loss_out), _ptr(workspace), _stream(stream)), 'sg_fwd_bwd')
+
+
+def adam_tf(params, m, v, grad, lr, beta1, beta2, eps, weight_decay, beta_powers, reg_loss=None,
+            stream=None):
+    check(lib().sg_adam_tf(_ptr(params), _ptr(m), _ptr(v), _ptr(grad), int(params.numel()),
+                           float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
+                           _ptr(beta_powers), _ptr(reg_loss), _stream(stream)), 'sg_adam_tf')

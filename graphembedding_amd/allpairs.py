@@ -1,0 +1,90 @@
+"""All-pairs Siamese training over a graph set (the BASELINE workload:
+AIDS700nef all-pairs, 700² = 490,000 ordered pairs per step).
+
+The pair stream is the ordered pair space p ↦ (p // G, p % G); each rank packs
+its contiguous shard once into HBM-resident pair records (sg_pack_pairs) and
+every step runs the fused fwd+bwd kernel over them, all-reduces the gradient
+(N > 1) and applies Adam.  Labels are y = exp(-η (2d/(n_i+n_j))²) from a GED
+matrix (synthetic offline).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+
+from .data import synthetic_ged_matrix, synthetic_graphs
+from .graphs import ModelGraph, NodeFeatureOneHotEncoder
+from .packer import GraphStore, pack_device, record_words
+from .shard import shard_range
+
+
+@dataclass
+class GraphSet:
+    graphs: list
+    mgs: List[ModelGraph]
+    d_in: int
+    n_max: int
+    store: GraphStore
+    ged: np.ndarray
+
+    def label_matrix(self, yeta: float, dist_norm: bool = True) -> np.ndarray:
+        sizes = np.array([g.number_of_nodes() for g in self.graphs], dtype=np.float64)
+        d = self.ged.astype(np.float64)
+        if dist_norm:
+            d = 2.0 * d / (sizes[:, None] + sizes[None, :])   # normalized_dist, distance.py:59-60
+        d = d.astype(np.float32).astype(np.float64)           # float32 placeholder feed
+        return np.exp(-yeta * d * d).astype(np.float32)
+
+    def flops_per_pair(self, h1=32, h2=16, D=10, K=10) -> float:
+        """Algorithmic FLOPs per pair, fwd+bwd (SURVEY §8(d) formula), averaged
+        over the all-pairs stream (every graph is g1 G times and g2 G times)."""
+        n = np.array([g.number_of_nodes() for g in self.graphs], dtype=np.float64)
+        e = np.array([g.number_of_edges() for g in self.graphs], dtype=np.float64)
+        nnz = n + 2 * e
+        fwd = 2 * h1 * n + 2 * h1 * nnz + 2 * n * h1 * h2 + 2 * h2 * nnz + 2 * n * h2
+        bwd = (2 * h1 * nnz + 2 * h1 * n) + (2 * h2 * nnz + 4 * n * h1 * h2) + 4 * n * h2
+        ntn_f = K * (4 * D + 2 * D * D + 2 * D)
+        return float(2 * (fwd + bwd).mean() + 3 * ntn_f)
+
+
+def load_graph_set(name: str = 'syn_aids700nef', n_max: int = 10, seed: int = 123) -> GraphSet:
+    tr, te = synthetic_graphs(name, seed)
+    graphs = tr + te
+    enc = NodeFeatureOneHotEncoder(graphs, 'type')
+    mgs = [ModelGraph(g, enc) for g in graphs]
+    store = GraphStore(mgs, n_max, enc.input_dim())
+    return GraphSet(graphs=graphs, mgs=mgs, d_in=enc.input_dim(), n_max=n_max, store=store,
+                    ged=synthetic_ged_matrix(graphs))
+
+
+class AllPairsShard(object):
+    """This rank's slice of the all-pairs stream, packed once into HBM."""
+
+    def __init__(self, gs: GraphSet, labels: np.ndarray, rank: int = 0, world: int = 1,
+                 device='cuda', n_pairs: Optional[int] = None):
+        import torch
+        G = len(gs.graphs)
+        self.total = int(n_pairs if n_pairs is not None else G * G)
+        self.start, self.end = shard_range(self.total, rank, world)
+        p = np.arange(self.start, self.end, dtype=np.int64)
+        pairs = np.stack([p // G, p % G], axis=1).astype(np.int32)
+        flat_labels = labels.reshape(-1)[:self.total]
+        lab = flat_labels[self.start:self.end]
+        self.records, status = pack_device(gs.store, pairs, lab, device=device)
+        torch.cuda.synchronize()
+        if int(status.item()) != 0:
+            raise RuntimeError('sg_pack_pairs reported invalid graph ids')
+        self.labels = torch.from_numpy(lab.copy()).to(device)
+        y = flat_labels.astype(np.float64)
+        ybar = y.mean()
+        self.y_stats = torch.tensor([ybar, 0.5 * ((y - ybar) ** 2).sum()], dtype=torch.float32,
+                                    device=device)
+        self.n = self.end - self.start
+        self.record_bytes = 4 * record_words(gs.n_max)
+
+    def batch(self, model, rank: int = 0):
+        return model.batch_from_records(self.records, self.n, self.labels,
+                                        pair_offset=self.start, batch_total=self.total,
+                                        y_stats=self.y_stats)

@@ -1,0 +1,133 @@
+// sg_common.h — shared device helpers of libsiamese_hip (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/siamese_hip.h"
+
+#define SG_WAVE 64
+
+// ---------------------------------------------------------------------------
+// Counter-based dropout RNG.  Bit-exact twin of oracle/siamese_oracle.py
+// (lowbias32, seed_key, dropout_mask).  Replaces TF's unseeded
+// floor(keep + U[0,1)) masks of layers.py:332-338 / tf.nn.dropout.
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint32_t sg_lowbias32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+static inline uint32_t sg_seed_key(uint64_t seed) {
+  const uint32_t lo = (uint32_t)(seed & 0xFFFFFFFFull);
+  const uint32_t hi = (uint32_t)(seed >> 32);
+  return (lo * 0x85EBCA6Bu) ^ hi;
+}
+
+static inline uint32_t sg_keep_threshold(float keep) {
+  if (keep >= 1.0f) return 65536u;
+  double t = (double)keep * 65536.0;
+  long r = (long)(t + 0.5);  // round half up == numpy round for these values
+  if (r < 0) r = 0;
+  if (r > 65536) r = 65536;
+  return (uint32_t)r;
+}
+
+__device__ __forceinline__ uint32_t sg_pair_key(uint32_t key, uint32_t pair) {
+  return sg_lowbias32(pair ^ key);
+}
+
+// One 32-bit hash serves two consecutive elements (e and e^1).
+__device__ __forceinline__ uint32_t sg_hash2(uint32_t pk, uint32_t layer, uint32_t side, uint32_t e) {
+  const uint32_t ctr = (layer << 26) | (side << 25) | (e >> 1);
+  return sg_lowbias32(ctr ^ pk);
+}
+
+__device__ __forceinline__ bool sg_keep(uint32_t pk, uint32_t layer, uint32_t side, uint32_t e,
+                                        uint32_t thr) {
+  if (thr >= 65536u) return true;
+  const uint32_t h = sg_hash2(pk, layer, side, e);
+  const uint32_t d = (e & 1u) ? (h >> 16) : (h & 0xFFFFu);
+  return d < thr;
+}
+
+// ---------------------------------------------------------------------------
+// Activations (layers_factory.py:101-114); gradients as TF's (ReluGrad: x>0).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float sg_act(int act, float x) {
+  switch (act) {
+    case SG_ACT_RELU: return x > 0.f ? x : 0.f;
+    case SG_ACT_SIGMOID: return 1.f / (1.f + __expf(-x));
+    case SG_ACT_TANH: return tanhf(x);
+    default: return x;
+  }
+}
+
+__device__ __forceinline__ float sg_act_grad(int act, float pre, float out, float g) {
+  switch (act) {
+    case SG_ACT_RELU: return pre > 0.f ? g : 0.f;
+    case SG_ACT_SIGMOID: return g * out * (1.f - out);
+    case SG_ACT_TANH: return g * (1.f - out * out);
+    default: return g;
+  }
+}
+
+// Final activation and its derivative (similarity.py:55-60, layers_factory.py:101-114).
+__device__ __forceinline__ float sg_final(int fa, float yeta, float s) {
+  switch (fa) {
+    case SG_FINAL_GAUSSIAN: return expf(-yeta * s * s);
+    case SG_FINAL_RELU: return s > 0.f ? s : 0.f;
+    case SG_FINAL_SIGMOID: return 1.f / (1.f + expf(-s));
+    case SG_FINAL_TANH: return tanhf(s);
+    default: return s;
+  }
+}
+
+__device__ __forceinline__ float sg_final_grad(int fa, float yeta, float s, float yhat) {
+  switch (fa) {
+    case SG_FINAL_GAUSSIAN: return -2.f * yeta * s * yhat;
+    case SG_FINAL_RELU: return s > 0.f ? 1.f : 0.f;
+    case SG_FINAL_SIGMOID: return yhat * (1.f - yhat);
+    case SG_FINAL_TANH: return 1.f - yhat * yhat;
+    default: return 1.f;
+  }
+}
+
+// Wave-local LDS hand-off: every prior LDS access of this wave has landed and
+// the compiler may not move memory operations across.
+__device__ __forceinline__ void sg_wsync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ float sg_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Pair record field offsets in 4-byte words (see siamese_hip.h).
+struct SgRecLayout {
+  int n_max;
+  int words;      // record size in 4-byte words
+  int adj;        // [2][n_max][n_max] f32
+  int types;      // [2][n_max] i32
+  int nnodes;     // [2] i32
+  int label;      // f32
+  int tag;        // i32
+};
+
+static inline SgRecLayout sg_rec_layout(int n_max) {
+  SgRecLayout r;
+  r.n_max = n_max;
+  r.adj = 0;
+  r.types = 2 * n_max * n_max;
+  r.nnodes = r.types + 2 * n_max;
+  r.label = r.nnodes + 2;
+  r.tag = r.label + 1;
+  r.words = r.tag + 1;
+  return r;
+}

@@ -1,0 +1,351 @@
+// siamese_hip.hip — C-ABI entry points of libsiamese_hip.so (include/siamese_hip.h)
+// plus the small kernels around the fused pair kernels: pair packing, label
+// statistics, the deterministic gradient-slab reduction and TF-form Adam.
+#include <mutex>
+
+#include "sg_plan.h"
+
+// ---------------------------------------------------------------------------
+// Device properties
+// ---------------------------------------------------------------------------
+int sg_num_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cache[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    cache[dev] = cus;
+  }
+  return cache[dev];
+}
+
+// generic path (sg_generic.hip)
+int sg_generic_lds_ok(const SgGenPlan &P, bool bwd);
+int64_t sg_generic_slab_floats(const SgGenPlan &P, int64_t n_pairs);
+int sg_generic_run(const SgGenPlan &P, bool bwd, const void *recs, int64_t n_pairs,
+                   int64_t pair_offset, int64_t batch_total, const float *params, uint64_t seed,
+                   const float *y_stats, float *s_out, float *slab, int *blocks_out,
+                   hipStream_t stream);
+// fused fast path (sg_fast.hip)
+int sg_fast_supported(const sg_model_t *m, const SgGenPlan &P);
+int64_t sg_fast_slab_floats(const SgGenPlan &P, int64_t n_pairs);
+int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
+                int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
+                uint64_t seed, const float *y_stats, float *s_out, float *slab, int *blocks_out,
+                hipStream_t stream);
+
+namespace {
+
+constexpr int kReduceStrands = 16;  // second-level partial rows
+
+// slab [nblk][C] → part [S][C]; strand order fixed ⇒ bitwise reproducible.
+__global__ void __launch_bounds__(256) sg_reduce_stage1(const float *__restrict__ slab, int nblk,
+                                                        int C, float *__restrict__ part) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  const int strand = blockIdx.y * 4 + w, nstrand = gridDim.y * 4;
+  float acc = 0.f;
+  if (col < C)
+    for (int b = strand; b < nblk; b += nstrand) acc += slab[(size_t)b * C + col];
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && col < C)
+    part[(size_t)blockIdx.y * C + col] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+// part [S][C] → grad[C-1], loss = part[:, C-1] (+ label term)
+__global__ void __launch_bounds__(256) sg_reduce_stage2(const float *__restrict__ part, int S, int C,
+                                                        float *__restrict__ grad,
+                                                        float *__restrict__ loss,
+                                                        const float *__restrict__ y_stats,
+                                                        int add_label) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= C) return;
+  float acc = 0.f;
+  for (int s = 0; s < S; ++s) acc += part[(size_t)s * C + col];
+  if (col < C - 1)
+    grad[col] = acc;
+  else if (loss)
+    loss[0] = acc + ((add_label && y_stats) ? y_stats[1] : 0.f);
+}
+
+// ---- label statistics (double accumulation) ----
+__global__ void __launch_bounds__(256) sg_label_partial(const uint8_t *__restrict__ recs, int64_t n,
+                                                        int rec_words, int label_off,
+                                                        const double *__restrict__ mean,
+                                                        double *__restrict__ part) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  const double mu = mean ? mean[0] : 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float y = ((const float *)(recs + (size_t)i * rec_words * 4u))[label_off];
+    const double d = (double)y - mu;
+    acc += mean ? d * d : (double)y;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(256) sg_label_final(const double *__restrict__ part, int np,
+                                                      int64_t n, int which, double *__restrict__ mean,
+                                                      float *__restrict__ stats) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < np; i += 256) acc += part[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (which == 0) {
+      const double mu = n > 0 ? red[0] / (double)n : 0.0;
+      mean[0] = mu;
+      stats[0] = (float)mu;
+    } else {
+      stats[1] = (float)(0.5 * red[0]);
+    }
+  }
+}
+
+// ---- pair packing: one wave per pair, record words copied lane-parallel ----
+__global__ void __launch_bounds__(256) sg_pack_kernel(const float *__restrict__ sadj,
+                                                      const int32_t *__restrict__ stypes,
+                                                      const int32_t *__restrict__ sn, int n_graphs,
+                                                      int nmax, const int32_t *__restrict__ pidx,
+                                                      const float *__restrict__ labels, int64_t n,
+                                                      uint32_t *__restrict__ recs, int rec_words,
+                                                      int32_t *__restrict__ status) {
+  const int lane = threadIdx.x & 63;
+  const int64_t p = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (p >= n) return;
+  const int g0 = pidx[2 * p], g1 = pidx[2 * p + 1];
+  const bool bad = g0 < 0 || g0 >= n_graphs || g1 < 0 || g1 >= n_graphs;
+  if (bad && lane == 0 && status) atomicExch(status, (int32_t)SG_ERR_ARG);
+  const int nn = nmax * nmax;
+  uint32_t *dst = recs + (size_t)p * rec_words;
+  for (int w = lane; w < rec_words; w += SG_WAVE) {
+    uint32_t v = 0u;
+    if (!bad) {
+      if (w < 2 * nn) {
+        const int s = w / nn, o = w - s * nn;
+        v = __float_as_uint(sadj[(size_t)(s ? g1 : g0) * nn + o]);
+      } else if (w < 2 * nn + 2 * nmax) {
+        const int o = w - 2 * nn, s = o / nmax, i = o - s * nmax;
+        v = (uint32_t)stypes[(size_t)(s ? g1 : g0) * nmax + i];
+      } else if (w < 2 * nn + 2 * nmax + 2) {
+        v = (uint32_t)sn[(w == 2 * nn + 2 * nmax) ? g0 : g1];
+      } else if (w == 2 * nn + 2 * nmax + 2) {
+        v = __float_as_uint(labels ? labels[p] : 0.f);
+      } else {
+        v = (uint32_t)(p & 0x7FFFFFFF);
+      }
+    }
+    dst[w] = v;
+  }
+}
+
+// ---- TF ApplyAdam (+ weight decay gradient) in one workgroup ----
+__global__ void __launch_bounds__(1024) sg_adam_kernel(float *__restrict__ th, float *__restrict__ m,
+                                                       float *__restrict__ v,
+                                                       const float *__restrict__ g, int64_t n,
+                                                       float lr, float b1, float b2, float eps,
+                                                       float wd, float *__restrict__ bp,
+                                                       float *__restrict__ reg_loss) {
+  __shared__ double red[1024];
+  const float b1p = bp[0], b2p = bp[1];
+  const float alpha = lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  const float c1 = 1.f - b1, c2 = 1.f - b2;
+  double reg = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) {
+    const float t = th[i];
+    reg += (double)t * (double)t;
+    const float gi = g[i] + wd * t;
+    const float mi = m[i] + (gi - m[i]) * c1;
+    const float vi = v[i] + (gi * gi - v[i]) * c2;
+    m[i] = mi;
+    v[i] = vi;
+    th[i] = t - (mi * alpha) / (sqrtf(vi) + eps);
+  }
+  red[threadIdx.x] = reg;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    bp[0] = b1p * b1;
+    bp[1] = b2p * b2;
+    if (reg_loss) reg_loss[0] = (float)((double)wd * 0.5 * red[0]);
+  }
+}
+
+int launch_reduce(const float *slab, int nblk, int C, float *part, float *grad, float *loss,
+                  const float *y_stats, int add_label, hipStream_t st) {
+  const int S = nblk < kReduceStrands ? (nblk > 0 ? nblk : 1) : kReduceStrands;
+  hipLaunchKernelGGL(sg_reduce_stage1, dim3((C + 63) / 64, S), dim3(256), 0, st, slab, nblk, C, part);
+  hipLaunchKernelGGL(sg_reduce_stage2, dim3((C + 255) / 256), dim3(256), 0, st, part, S, C, grad,
+                     loss, y_stats, add_label);
+  return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
+}
+
+struct PathChoice {
+  int status;
+  bool fast;
+  SgGenPlan plan;
+};
+
+PathChoice choose_path(const sg_model_t *m, bool bwd) {
+  PathChoice c;
+  c.status = sg_build_plan(m, &c.plan);
+  c.fast = false;
+  if (c.status != SG_OK) return c;
+  if (sg_fast_supported(m, c.plan)) {
+    c.fast = true;
+    return c;
+  }
+  if (!sg_generic_lds_ok(c.plan, bwd)) c.status = SG_ERR_UNSUPPORTED;
+  return c;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" {
+
+int32_t sg_version(void) { return 10000; }
+
+int64_t sg_record_bytes(int32_t n_max) {
+  if (n_max <= 0) return 0;
+  return (int64_t)sg_rec_layout(n_max).words * 4;
+}
+
+int32_t sg_model_validate(const sg_model_t *model, int64_t *n_params_out, int32_t *path_out) {
+  PathChoice c = choose_path(model, true);
+  if (c.status != SG_OK) return c.status;
+  if (n_params_out) *n_params_out = c.plan.n_params;
+  if (path_out) *path_out = c.fast ? 1 : 0;
+  return SG_OK;
+}
+
+int64_t sg_workspace_bytes(const sg_model_t *model, int64_t n_pairs) {
+  PathChoice c = choose_path(model, true);
+  if (c.status != SG_OK) return -1;
+  const int64_t C = c.plan.n_params + 1;
+  const int64_t slab = c.fast ? sg_fast_slab_floats(c.plan, n_pairs)
+                              : sg_generic_slab_floats(c.plan, n_pairs);
+  int64_t bytes = (slab + (int64_t)kReduceStrands * C) * 4;
+  bytes = (bytes + 255) & ~(int64_t)255;
+  const int64_t label_bytes = (256 + 2) * 8;
+  return (bytes > label_bytes ? bytes : label_bytes) + 256;
+}
+
+int32_t sg_pack_pairs(const float *store_adj, const int32_t *store_types, const int32_t *store_n,
+                      int32_t n_graphs, int32_t n_max, const int32_t *pair_idx,
+                      const float *labels, int64_t n_pairs, void *records,
+                      int32_t *status_out, sg_stream_t stream) {
+  if (n_pairs < 0 || n_max <= 0 || n_max > 64 || n_graphs <= 0) return SG_ERR_ARG;
+  if (n_pairs == 0) return SG_OK;
+  if (!store_adj || !store_types || !store_n || !pair_idx || !records) return SG_ERR_ARG;
+  const SgRecLayout rl = sg_rec_layout(n_max);
+  const int wpb = 4;
+  const int64_t blocks = (n_pairs + wpb - 1) / wpb;
+  if (blocks > 0x7FFFFFFF) return SG_ERR_ARG;
+  hipLaunchKernelGGL(sg_pack_kernel, dim3((unsigned)blocks), dim3(64 * wpb), 0, (hipStream_t)stream,
+                     store_adj, store_types, store_n, n_graphs, n_max, pair_idx, labels, n_pairs,
+                     (uint32_t *)records, rl.words, status_out);
+  return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
+}
+
+int32_t sg_label_stats(const void *records, int64_t n_pairs, int32_t n_max, float *stats_out,
+                       void *workspace, sg_stream_t stream) {
+  if (!records || !stats_out || !workspace || n_pairs <= 0 || n_max <= 0 || n_max > 64)
+    return SG_ERR_ARG;
+  const SgRecLayout rl = sg_rec_layout(n_max);
+  hipStream_t st = (hipStream_t)stream;
+  double *part = (double *)workspace;
+  double *mean = part + 256;
+  const int nb = 256;
+  hipLaunchKernelGGL(sg_label_partial, dim3(nb), dim3(256), 0, st, (const uint8_t *)records,
+                     n_pairs, rl.words, rl.label, (const double *)nullptr, part);
+  hipLaunchKernelGGL(sg_label_final, dim3(1), dim3(256), 0, st, part, nb, n_pairs, 0, mean,
+                     stats_out);
+  hipLaunchKernelGGL(sg_label_partial, dim3(nb), dim3(256), 0, st, (const uint8_t *)records,
+                     n_pairs, rl.words, rl.label, (const double *)mean, part);
+  hipLaunchKernelGGL(sg_label_final, dim3(1), dim3(256), 0, st, part, nb, n_pairs, 1, mean,
+                     stats_out);
+  return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
+}
+
+int32_t sg_forward(const sg_model_t *model, const void *records, int64_t n_pairs,
+                   int64_t pair_offset, const float *params, uint64_t seed, float *s_out,
+                   void *workspace, sg_stream_t stream) {
+  (void)workspace;
+  if (n_pairs < 0 || pair_offset < 0) return SG_ERR_ARG;
+  if (n_pairs == 0) return SG_OK;
+  if (!records || !params || !s_out) return SG_ERR_ARG;
+  PathChoice c = choose_path(model, false);
+  if (c.status != SG_OK) return c.status;
+  if (c.fast)
+    return sg_fast_run(model, c.plan, false, records, n_pairs, pair_offset, n_pairs, params, seed,
+                       nullptr, s_out, nullptr, nullptr, (hipStream_t)stream);
+  return sg_generic_run(c.plan, false, records, n_pairs, pair_offset, n_pairs, params, seed,
+                        nullptr, s_out, nullptr, nullptr, (hipStream_t)stream);
+}
+
+int32_t sg_fwd_bwd(const sg_model_t *model, const void *records, int64_t n_pairs,
+                   int64_t pair_offset, int64_t batch_total, const float *params, uint64_t seed,
+                   const float *y_stats, int32_t add_label_term, float *s_out, float *grad_out,
+                   float *loss_out, void *workspace, sg_stream_t stream) {
+  if (n_pairs < 0 || pair_offset < 0) return SG_ERR_ARG;
+  if (!params || !grad_out || !workspace) return SG_ERR_ARG;
+  PathChoice c = choose_path(model, true);
+  if (c.status != SG_OK) return c.status;
+  if (model->loss_mode == SG_LOSS_BROADCAST && !y_stats) return SG_ERR_ARG;
+  if (model->loss_mode == SG_LOSS_ALIGNED && batch_total <= 0) return SG_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const int C = c.plan.n_params + 1;
+  float *slab = (float *)workspace;
+  if (n_pairs == 0) {
+    if (hipMemsetAsync(grad_out, 0, (size_t)c.plan.n_params * 4u, st) != hipSuccess)
+      return SG_ERR_HIP;
+    if (loss_out && hipMemsetAsync(loss_out, 0, 4u, st) != hipSuccess) return SG_ERR_HIP;
+    return SG_OK;
+  }
+  if (!records) return SG_ERR_ARG;
+  int nblk = 0;
+  int rc;
+  if (c.fast)
+    rc = sg_fast_run(model, c.plan, true, records, n_pairs, pair_offset, batch_total, params, seed,
+                     y_stats, s_out, slab, &nblk, st);
+  else
+    rc = sg_generic_run(c.plan, true, records, n_pairs, pair_offset, batch_total, params, seed,
+                        y_stats, s_out, slab, &nblk, st);
+  if (rc != SG_OK) return rc;
+  float *part = slab + (size_t)nblk * C;
+  return launch_reduce(slab, nblk, C, part, grad_out, loss_out, y_stats,
+                       model->loss_mode == SG_LOSS_BROADCAST ? add_label_term : 0, st);
+}
+
+int32_t sg_adam_tf(float *params, float *m, float *v, const float *grad, int64_t n, float lr,
+                   float beta1, float beta2, float eps, float weight_decay, float *beta_powers,
+                   float *reg_loss_out, sg_stream_t stream) {
+  if (!params || !m || !v || !grad || !beta_powers || n <= 0) return SG_ERR_ARG;
+  hipLaunchKernelGGL(sg_adam_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, params, m, v,
+                     grad, n, lr, beta1, beta2, eps, weight_decay, beta_powers, reg_loss_out);
+  return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
+}
+
+}  // extern "C"

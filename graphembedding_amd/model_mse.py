@@ -1,0 +1,271 @@
+"""SiameseGCNTNMSE — host mirror of model/Siamese/model_mse.py:9-168 +
+models.py:6-131 on top of the HIP C-ABI.
+
+What was `sess.run` in the reference is now a sequence of stream-ordered
+C-ABI calls on torch's current stream:
+  train  (train.py:85)  sg_fwd_bwd → [all-reduce] → sg_adam_tf
+  val    (train.py:86)  sg_fwd_bwd (loss only)
+  test   (train.py:87)  sg_forward → pre-activation s (pred_sim_without_act)
+Parameters are one flat fp32 device vector in the reference's variable order.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from .config import FLAGS
+from .layers_factory import create_activation, create_layers, padding_dims
+from .packer import GraphStore, record_words
+from .similarity import create_sim_kernel
+
+
+def param_shapes(layers: List[dict], d_in: int) -> List[Tuple[int, str, Tuple[int, ...]]]:
+    """(layer index, variable name, shape) in variable creation order
+    (layers.py:68-73, 151-152, 174-178, 268-277)."""
+    out = []
+    for li, L in enumerate(layers):
+        k = L['kind']
+        if k == 'GraphConvolution':
+            din = L.get('input_dim') or d_in
+            out.append((li, 'weights_0', (din, L['output_dim'])))
+            if L['bias']:
+                out.append((li, 'bias', (L['output_dim'],)))
+        elif k == 'Dense':
+            out.append((li, 'weights', (L['input_dim'], L['output_dim'])))
+            if L['bias']:
+                out.append((li, 'bias', (L['output_dim'],)))
+        elif k == 'Attention':
+            out.append((li, 'weights', (L['input_dim'], L['input_dim'])))
+        elif k == 'NTN':
+            D, K = L['input_dim'], L['feature_map_dim']
+            out += [(li, 'weights_W', (D, D, K)), (li, 'weights_V', (K, 2 * D)),
+                    (li, 'weights_U', (K, 1))]
+            if L['bias']:
+                out.append((li, 'bias', (K,)))
+    return out
+
+
+def glorot_flat(layers: List[dict], d_in: int, seed: int = 0) -> np.ndarray:
+    """inits.py:11-21 (uniform ±√(6/(s0+s1)); zeros for biases), numpy-seeded."""
+    rng = np.random.default_rng(seed)
+    parts = []
+    for li, name, shape in param_shapes(layers, d_in):
+        if name == 'bias':
+            parts.append(np.zeros(shape))
+        else:
+            r = math.sqrt(6.0 / (shape[0] + shape[1]))
+            parts.append(rng.uniform(-r, r, size=shape))
+    return np.concatenate([p.ravel() for p in parts]).astype(np.float32)
+
+
+@dataclass
+class Batch:
+    """A packed batch resident on the device (what get_feed_dict returns)."""
+    records: object                 # torch.int32 [n * record_words]
+    n_pairs: int
+    labels: object                  # torch.float32 [n] (per input pair, for aligned loss)
+    y_stats: object                 # torch.float32 [2] {ȳ, ½Σ(y-ȳ)²} of the label set
+    pair_offset: int = 0            # global index of record 0 (dropout RNG / sharding)
+    batch_total: int = 0            # global batch size B
+    gid_pairs: Optional[np.ndarray] = None
+
+
+class SiameseGCNTNMSE(object):
+    def __init__(self, input_dim, flags=None, device='cuda', n_max=None, params=None):
+        f = flags or FLAGS
+        assert f.loss_func == 'mse'
+        self.flags = f
+        self.input_dim = int(input_dim)
+        self.device = device
+        self.layers = create_layers(f, self.input_dim)
+        pd = padding_dims(self.layers)
+        self.n_max = int(n_max or f.n_max or pd or 10)
+        if pd is not None and self.n_max > pd:
+            # records may hold up to n_max nodes; the reference's tf.pad requires N <= pd
+            pass
+        self.sim_kernel = create_sim_kernel(f.sim_kernel, f.yeta)
+        self.final_act_np = create_activation(f.final_act, self.sim_kernel)
+        self.sg = _lib.make_model(self.layers, self.input_dim, self.n_max, 1.0 - f.dropout,
+                                  f.final_act, f.sim_kernel, f.yeta, f.loss_mode, f.ntn_mode)
+        self.n_params, self.kernel_path = _lib.validate(self.sg)
+        import torch
+        self.torch = torch
+        init = glorot_flat(self.layers, self.input_dim, f.param_seed) if params is None else \
+            np.asarray(params, np.float32)
+        assert init.shape[0] == self.n_params, (init.shape, self.n_params)
+        self.params = torch.from_numpy(init.copy()).to(device)
+        self.adam_m = torch.zeros_like(self.params)
+        self.adam_v = torch.zeros_like(self.params)
+        self.beta1, self.beta2, self.eps = 0.9, 0.999, 1e-8
+        self.beta_powers = torch.tensor([self.beta1, self.beta2], dtype=torch.float32, device=device)
+        self.grad = torch.zeros_like(self.params)
+        self.loss_buf = torch.zeros(2, dtype=torch.float32, device=device)
+        self.reg_buf = torch.zeros(1, dtype=torch.float32, device=device)
+        self._ws = None
+        self._ws_pairs = -1
+        self.seed = int(f.seed)
+        self.step_count = 0
+        self.grad_hook = None   # e.g. the data-parallel all-reduce (shard.py)
+
+    # ---- reference API ------------------------------------------------------
+    def apply_final_act_np(self, score):
+        return self.final_act_np(score)
+
+    def pred_sim_without_act(self, batch: Batch, seed: Optional[int] = None):
+        """Pre-activation scores of the batch (train.py:87 'test')."""
+        torch = self.torch
+        s = torch.empty(batch.n_pairs, dtype=torch.float32, device=self.device)
+        _lib.forward(self.sg, batch.records, batch.n_pairs, batch.pair_offset, self.params,
+                     self._seed(seed), s)
+        return s
+
+    def get_feed_dict(self, data, dist_calculator, tvt, test_id=None, train_id=None):
+        """model_mse.py:52-94, same sampler-call pattern (quirk A3 in 'compat')."""
+        B = self.flags.batch_size
+        if tvt in ('train', 'val'):
+            assert test_id is None and train_id is None
+            pairs = [data.get_graph_pair(tvt) for _ in range(B)]
+        else:
+            assert tvt == 'test'
+            pairs = [(data.test_data.get_graph(test_id), data.get_orig_train_graph(train_id))]
+        dists = norm_dists = None
+        if tvt in ('train', 'val'):
+            if self.flags.label_stream == 'compat':
+                # the label block sits inside the per-pair loop: B redraws of B pairs
+                for _ in range(len(pairs)):
+                    dists, norm_dists = np.zeros(B), np.zeros(B)
+                    for i in range(B):
+                        g1, g2 = data.get_graph_pair(tvt)
+                        d, nd = data.get_dist(g1.get_nxgraph(), g2.get_nxgraph(), dist_calculator)
+                        dists[i], norm_dists[i] = d, nd
+            else:
+                dists, norm_dists = np.zeros(B), np.zeros(B)
+                for i, (g1, g2) in enumerate(pairs):
+                    d, nd = data.get_dist(g1.get_nxgraph(), g2.get_nxgraph(), dist_calculator)
+                    dists[i], norm_dists[i] = d, nd
+        labels = None
+        if dists is not None:
+            d = norm_dists if self.flags.dist_norm else dists
+            labels = self.sim_kernel.dist_to_sim_np(np.asarray(d, np.float32).astype(np.float64))
+        return self.make_batch([p[0] for p in pairs], [p[1] for p in pairs], labels)
+
+    def make_batch(self, g1s: Sequence, g2s: Sequence, labels=None, pair_offset=0,
+                   batch_total=None) -> Batch:
+        """Pack ModelGraph pairs on the host and move them to the device."""
+        torch = self.torch
+        uniq, index = [], {}
+        idx = np.zeros((len(g1s), 2), np.int32)
+        for k, (a, b) in enumerate(zip(g1s, g2s)):
+            for c, g in enumerate((a, b)):
+                if id(g) not in index:
+                    index[id(g)] = len(uniq)
+                    uniq.append(g)
+                idx[k, c] = index[id(g)]
+        store = GraphStore(uniq, self.n_max, self.input_dim)
+        lab = np.zeros(len(g1s), np.float32) if labels is None else np.asarray(labels, np.float32)
+        words = store.pack_host(idx, lab)
+        recs = torch.from_numpy(words.view(np.int32).reshape(-1)).to(self.device)
+        gids = np.array([[a.nxgraph.graph.get('gid', -1), b.nxgraph.graph.get('gid', -1)]
+                         for a, b in zip(g1s, g2s)])
+        return self.batch_from_records(recs, len(g1s), lab, pair_offset, batch_total, gids)
+
+    def batch_from_records(self, recs, n_pairs, labels, pair_offset=0, batch_total=None,
+                           gid_pairs=None, y_stats=None) -> Batch:
+        torch = self.torch
+        lab = torch.as_tensor(np.asarray(labels, np.float32) if not torch.is_tensor(labels)
+                              else labels, dtype=torch.float32, device=self.device)
+        if y_stats is None:
+            y64 = lab.double()
+            ybar = y64.mean() if n_pairs else torch.zeros((), dtype=torch.float64,
+                                                          device=self.device)
+            half = 0.5 * ((y64 - ybar) ** 2).sum()
+            y_stats = torch.stack([ybar, half]).float()
+        return Batch(records=recs, n_pairs=int(n_pairs), labels=lab, y_stats=y_stats,
+                     pair_offset=int(pair_offset),
+                     batch_total=int(batch_total if batch_total is not None else n_pairs),
+                     gid_pairs=gid_pairs)
+
+    # ---- steps ----------------------------------------------------------------
+    def _seed(self, seed):
+        return (self.seed * 1000003 + self.step_count) if seed is None else int(seed)
+
+    def workspace(self, n_pairs):
+        torch = self.torch
+        if self._ws is None or n_pairs > self._ws_pairs:
+            nbytes = _lib.workspace_bytes(self.sg, max(int(n_pairs), 1))
+            self._ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device=self.device)
+            self._ws_pairs = int(n_pairs)
+        return self._ws
+
+    def fwd_bwd(self, batch: Batch, seed=None, s_out=None, add_label_term=True):
+        """Forward + loss + backward; leaves Σ∂loss_mse/∂θ in self.grad and the
+        shard's loss_mse in self.loss_buf[0]."""
+        _lib.fwd_bwd(self.sg, batch.records, batch.n_pairs, batch.pair_offset,
+                     batch.batch_total, self.params, self._seed(seed), batch.y_stats,
+                     1 if add_label_term else 0, s_out, self.grad, self.loss_buf,
+                     self.workspace(batch.n_pairs))
+
+    def apply_adam(self):
+        f = self.flags
+        _lib.adam_tf(self.params, self.adam_m, self.adam_v, self.grad, f.learning_rate,
+                     self.beta1, self.beta2, self.eps, f.weight_decay, self.beta_powers,
+                     self.reg_buf)
+
+    def train_step(self, batch: Batch, seed=None, sync=True):
+        """sess.run([opt_op, loss]) (train.py:85,92): returns the loss evaluated
+        at the pre-update parameters (incl. weight decay, models.py:67-88)."""
+        self.fwd_bwd(batch, seed)
+        if self.grad_hook is not None:
+            self.grad_hook(self)
+        self.apply_adam()
+        self.step_count += 1
+        if not sync:
+            return None
+        return float(self.loss_buf[0].item() + self.reg_buf[0].item())
+
+    def val_loss(self, batch: Batch, seed=None):
+        self.fwd_bwd(batch, seed)
+        reg = self.flags.weight_decay * 0.5 * float((self.params.double() ** 2).sum().item())
+        return float(self.loss_buf[0].item()) + reg
+
+    def test_scores(self, batch: Batch, seed=None):
+        return self.pred_sim_without_act(batch, seed).cpu().numpy().astype(np.float64)
+
+    def flat_params(self) -> np.ndarray:
+        return self.params.detach().cpu().numpy()
+
+    def set_params(self, flat):
+        self.params.copy_(self.torch.as_tensor(np.asarray(flat, np.float32)))
+
+    # ---- checkpoint / resume (models.py:118-131 counterpart) -------------------
+    def state_dict(self):
+        return dict(params=self.params.cpu(), adam_m=self.adam_m.cpu(), adam_v=self.adam_v.cpu(),
+                    beta_powers=self.beta_powers.cpu(),
+                    step_count=self.torch.tensor(self.step_count))
+
+    def load_state_dict(self, sd):
+        self.params.copy_(sd['params'])
+        self.adam_m.copy_(sd['adam_m'])
+        self.adam_v.copy_(sd['adam_v'])
+        self.beta_powers.copy_(sd['beta_powers'])
+        self.step_count = int(sd['step_count'])
+
+    def save(self, path):
+        self.torch.save(self.state_dict(), path)
+
+    def load(self, path):
+        self.load_state_dict(self.torch.load(path, weights_only=True))
+
+
+def create_model(model, input_dim, flags=None, **kw):
+    """models_factory.py:5-11."""
+    if model == 'siamese_gcntn_mse':
+        return SiameseGCNTNMSE(input_dim, flags, **kw)
+    elif model == 'siamese_gcntn_hinge':
+        raise RuntimeError('siamese_gcntn_hinge is an unimplemented stub in the reference '
+                           '(model_hinge.py:5-45)')
+    raise RuntimeError('Unknown model {}'.format(model))

@@ -1,0 +1,189 @@
+/*
+ * siamese_hip.h — C-ABI of libsiamese_hip.so, the MI355X (gfx950) hot path of
+ * the Siamese GCN → pooling → NTN → Gaussian-similarity → MSE model of
+ * kangzf/GraphEmbedding (model/Siamese).
+ *
+ * The reference has no FFI: its hot path is the TensorFlow 1.x graph executed by
+ * `sess.run` at model/Siamese/train.py:92, fed by
+ * SiameseGCNTNMSE.get_feed_dict (model/Siamese/model_mse.py:52-94).  Each entry
+ * point below replaces one piece of that `sess.run`, called from the host mirror
+ * graphembedding_amd/model_mse.py via ctypes:
+ *
+ *   sg_pack_pairs    get_feed_dict's per-pair sparse-tuple feeds
+ *                    (model_mse.py:65-81) → one packed pair record per pair.
+ *   sg_forward       sess.run([model.pred_sim_without_act()])  (train.py:87,92;
+ *                    models.py:90-91) — pre-activation score s per pair.
+ *   sg_fwd_bwd       the forward + MSE loss + autodiff of
+ *                    sess.run([opt_op, loss])  (train.py:85,92; models.py:34-36;
+ *                    model_mse.py:145-151), gradient summed over the batch.
+ *   sg_adam_tf       AdamOptimizer(lr).minimize's ApplyAdam update incl. the
+ *                    weight-decay term of models.py:67-73.
+ *   sg_label_stats   the label side of the B×B broadcast loss
+ *                    (model_mse.py:148-151): mean label and ½Σ(y-ȳ)².
+ *
+ * Conventions: every pointer is a caller-owned DEVICE buffer unless noted;
+ * every call is stream-ordered on `stream` (a hipStream_t, 0 = null stream),
+ * performs no allocation and no host synchronisation, and returns SG_OK (0) or
+ * an SG_ERR_* code.  Calls are thread-compatible (one stream per caller).
+ */
+#ifndef SIAMESE_HIP_H
+#define SIAMESE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *sg_stream_t; /* hipStream_t */
+
+enum sg_status {
+  SG_OK = 0,
+  SG_ERR_ARG = 1,          /* invalid argument / inconsistent model (reference: RuntimeError) */
+  SG_ERR_UNSUPPORTED = 2,  /* valid reference model this build has no kernel for */
+  SG_ERR_HIP = 3,          /* a HIP runtime call failed */
+  SG_ERR_SHAPE = 4         /* e.g. Padding with N > max_in_dims (tf.pad error, layers.py:226) */
+};
+
+/* Layer kinds of the layer-string grammar (layers_factory.py:8-34). */
+enum sg_layer_kind {
+  SG_GCN = 1,       /* GraphConvolution   layers.py:52-118  */
+  SG_DENSE = 2,     /* Dense              layers.py:163-205 */
+  SG_PADDING = 3,   /* Padding            layers.py:208-227 */
+  SG_AVERAGE = 4,   /* Average            layers.py:121-140 */
+  SG_ATTENTION = 5, /* Attention          layers.py:143-160 (dead code in the reference; build option) */
+  SG_NTN = 6,       /* NTN                layers.py:255-310 */
+  SG_DOT = 7        /* Dot                layers.py:230-252 */
+};
+
+/* Activations (layers_factory.py:101-114). */
+enum sg_act { SG_ACT_IDENTITY = 0, SG_ACT_RELU = 1, SG_ACT_SIGMOID = 2, SG_ACT_TANH = 3 };
+
+/* Final activation (config.py:81-83 FLAGS.final_act with FLAGS.sim_kernel). */
+enum sg_final {
+  SG_FINAL_GAUSSIAN = 0, /* 'sim_kernel' with 'gaussian': exp(-yeta s^2) (similarity.py:58-60) */
+  SG_FINAL_IDENTITY = 1, /* 'identity', or 'sim_kernel' with 'identity' */
+  SG_FINAL_RELU = 2,
+  SG_FINAL_SIGMOID = 3,
+  SG_FINAL_TANH = 4
+};
+
+enum sg_loss_mode {
+  SG_LOSS_BROADCAST = 0, /* reference quirk A2: l2_loss((B,1)-(B,))/B */
+  SG_LOSS_ALIGNED = 1    /* per-pair MSE: ½Σ(y_i-ŷ_i)²/B */
+};
+
+enum sg_ntn_mode {
+  SG_NTN_REFERENCE = 0, /* quirk A1: s = (ΣU)·Σ_k act(m_k)  (layers.py:305-308) */
+  SG_NTN_INTENDED = 1   /* s = Σ_k U_k act(m_k) */
+};
+
+#define SG_MAX_LAYERS 8
+
+typedef struct sg_layer {
+  int32_t kind;          /* sg_layer_kind */
+  int32_t input_dim;     /* GCN/Dense/Attention/NTN input width (GCN layer 0: d_in) */
+  int32_t output_dim;    /* GCN/Dense output; NTN feature_map_dim; Padding max_in_dims */
+  int32_t act;           /* sg_act (GCN/Dense act, NTN inneract) */
+  int32_t bias;          /* 0/1 */
+  int32_t dropout;       /* 0/1: layer reads FLAGS.dropout (layers.py:45-49) */
+  int32_t sparse_inputs; /* GCN: 1 for the one-hot feature layer */
+  float padding_value;   /* Padding */
+} sg_layer_t;
+
+typedef struct sg_model {
+  int32_t num_layers;
+  int32_t d_in;       /* one-hot width = NodeFeatureOneHotEncoder.input_dim() */
+  int32_t n_max;      /* node capacity of one graph slot of a pair record */
+  int32_t final_act;  /* sg_final */
+  int32_t loss_mode;  /* sg_loss_mode */
+  int32_t ntn_mode;   /* sg_ntn_mode */
+  float keep_prob;    /* 1 - FLAGS.dropout */
+  float yeta;         /* FLAGS.yeta */
+  sg_layer_t layers[SG_MAX_LAYERS];
+} sg_model_t;
+
+/*
+ * Packed pair record (fp32), little-endian, 16-byte aligned, one per pair:
+ *   float   adj[2][n_max][n_max];   Â of graph 1 / graph 2, rows/cols >= n zero
+ *   int32_t types[2][n_max];        one-hot column of each node (graphs.py:108-111)
+ *   int32_t n_nodes[2];
+ *   float   label;                  y = sim_kernel(norm_dist) of the pair (aligned loss)
+ *   int32_t tag;                    free (host bookkeeping: source pair index)
+ * sg_record_bytes(10) == 896.
+ */
+int64_t sg_record_bytes(int32_t n_max);
+
+/* Library version (major*10000 + minor*100 + patch). */
+int32_t sg_version(void);
+
+/*
+ * Validate a model against the reference grammar and this build's kernels.
+ * n_params_out: length of the flat fp32 parameter vector (variables in layer
+ * order: GCN weights_0,bias; Dense weights,bias; Attention weights;
+ * NTN weights_W[D][D][K], weights_V[K][2D], weights_U[K][1], bias[K]).
+ * path_out: 1 = fused MFMA fast path, 0 = generic path.  Host-only, no GPU.
+ */
+int32_t sg_model_validate(const sg_model_t *model, int64_t *n_params_out, int32_t *path_out);
+
+/* Workspace bytes needed by sg_forward / sg_fwd_bwd / sg_label_stats for n_pairs. */
+int64_t sg_workspace_bytes(const sg_model_t *model, int64_t n_pairs);
+
+/*
+ * Gather pair records from a device graph store.
+ *   store_adj   [n_graphs][n_max][n_max] f32, store_types [n_graphs][n_max] i32,
+ *   store_n     [n_graphs] i32, pair_idx [n_pairs][2] i32 (graph ids),
+ *   labels      [n_pairs] f32 or NULL (label := 0), records out.
+ * Invalid graph ids give SG_ERR_ARG in *status_out (device int, may be NULL).
+ */
+int32_t sg_pack_pairs(const float *store_adj, const int32_t *store_types, const int32_t *store_n,
+                      int32_t n_graphs, int32_t n_max, const int32_t *pair_idx,
+                      const float *labels, int64_t n_pairs, void *records,
+                      int32_t *status_out, sg_stream_t stream);
+
+/* stats_out[0] = mean label ȳ, stats_out[1] = ½Σ(y-ȳ)² over the n_pairs records. */
+int32_t sg_label_stats(const void *records, int64_t n_pairs, int32_t n_max, float *stats_out,
+                       void *workspace, sg_stream_t stream);
+
+/*
+ * Forward only: s_out[i] = pre-activation score of record i (the test path:
+ * pred_sim_without_act, train.py:87).  Dropout masks are keyed by
+ * (seed, pair_offset + i) so a sharded batch reproduces the unsharded one.
+ */
+int32_t sg_forward(const sg_model_t *model, const void *records, int64_t n_pairs,
+                   int64_t pair_offset, const float *params, uint64_t seed, float *s_out,
+                   void *workspace, sg_stream_t stream);
+
+/*
+ * Forward + loss + backward over n_pairs records.
+ *   y_stats     device [2] = {ȳ, ½Σ(y-ȳ)²} of the WHOLE batch (broadcast loss);
+ *               ignored in aligned mode.
+ *   batch_total global batch size B (aligned loss divides by it).
+ *   grad_out    [n_params] Σ_pairs ∂loss_mse/∂θ (no weight decay; that is added
+ *               by sg_adam_tf so that a multi-GPU all-reduce sums it once).
+ *   loss_out    [1] this shard's loss_mse contribution: ½Σ_j(ŷ_j-ȳ)² (+ ½Σ(y-ȳ)²
+ *               when add_label_term != 0) in broadcast mode, ½Σ(y-ŷ)²/B aligned.
+ *   s_out       [n_pairs] or NULL.
+ */
+int32_t sg_fwd_bwd(const sg_model_t *model, const void *records, int64_t n_pairs,
+                   int64_t pair_offset, int64_t batch_total, const float *params, uint64_t seed,
+                   const float *y_stats, int32_t add_label_term, float *s_out, float *grad_out,
+                   float *loss_out, void *workspace, sg_stream_t stream);
+
+/*
+ * TF ApplyAdam (training_ops ApplyAdam, non-Nesterov) with the weight-decay
+ * gradient wd·θ added first (models.py:69-73):
+ *   g = grad + wd·θ; α = lr·√(1-β2^t)/(1-β1^t); m += (g-m)(1-β1);
+ *   v += (g²-v)(1-β2); θ -= α·m/(√v+ε); then β1^t *= β1, β2^t *= β2.
+ * beta_powers: device [2] {β1^t, β2^t}, initialised by the caller to {β1, β2}.
+ * reg_loss_out: device [1] or NULL: wd·½Σθ² of the parameters BEFORE the update.
+ */
+int32_t sg_adam_tf(float *params, float *m, float *v, const float *grad, int64_t n, float lr,
+                   float beta1, float beta2, float eps, float weight_decay, float *beta_powers,
+                   float *reg_loss_out, sg_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIAMESE_HIP_H */

@@ -1,0 +1,107 @@
+"""Shared test fixtures: small synthetic AIDS-shaped problems, the oracle twin
+of the GPU model, and helpers to run both on identical inputs."""
+from __future__ import annotations
+
+import os
+import sys
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+from graphembedding_amd.config import Flags  # noqa: E402
+from graphembedding_amd.data import synthetic_graph  # noqa: E402
+from graphembedding_amd.graphs import ModelGraph, NodeFeatureOneHotEncoder  # noqa: E402
+from graphembedding_amd.layers_factory import create_layers  # noqa: E402
+from graphembedding_amd.model_mse import glorot_flat  # noqa: E402
+from graphembedding_amd.packer import GraphStore  # noqa: E402
+from oracle import siamese_oracle as O  # noqa: E402
+
+AVERAGE_STACK = dict(
+    num_layers=4,
+    layer_0='GraphConvolution:output_dim=32,act=relu,dropout=True,bias=True,sparse_inputs=True',
+    layer_1='GraphConvolution:input_dim=32,output_dim=16,act=identity,dropout=True,bias=True,'
+            'sparse_inputs=False',
+    layer_2='Average',
+    layer_3='NTN:input_dim=16,feature_map_dim=10,inneract=relu,dropout=True,bias=True')
+
+
+@dataclass
+class Problem:
+    flags: Flags
+    graphs: list                    # networkx graphs
+    mgs: List[ModelGraph]
+    d_in: int
+    n_max: int
+    pairs: np.ndarray               # [P, 2] graph indices
+    labels: np.ndarray              # [P] float32 similarities
+    params: np.ndarray              # float32 flat
+    layers: list = field(default_factory=list)
+
+    def oracle_spec(self) -> O.OracleSpec:
+        f = self.flags
+        return O.OracleSpec(layers=self.layers, d_in=self.d_in, keep_prob=1.0 - f.dropout,
+                            final_act=f.final_act, sim_kernel=f.sim_kernel, yeta=f.yeta,
+                            loss_mode=f.loss_mode, ntn_mode=f.ntn_mode,
+                            weight_decay=f.weight_decay, dist_norm=f.dist_norm)
+
+    def oracle_graphs(self):
+        gs = [O.Graph(adj=m.adj.astype(np.float32).astype(np.float64), types=m.types)
+              for m in self.mgs]
+        return [gs[i] for i in self.pairs[:, 0]], [gs[j] for j in self.pairs[:, 1]]
+
+    def store(self) -> GraphStore:
+        return GraphStore(self.mgs, self.n_max, self.d_in)
+
+    def make_gpu_model(self, device='cuda'):
+        from graphembedding_amd.model_mse import SiameseGCNTNMSE
+        import torch
+        model = SiameseGCNTNMSE(self.d_in, self.flags, device=device, n_max=self.n_max,
+                                params=self.params)
+        words = self.store().pack_host(self.pairs, self.labels)
+        recs = torch.from_numpy(words.view(np.int32).reshape(-1)).to(device)
+        batch = model.batch_from_records(recs, len(self.pairs), self.labels)
+        return model, batch
+
+
+def small_problem(n_graphs=12, n_pairs=24, seed=5, n_lo=3, n_hi=10, n_max=10, n_types=29,
+                  flags_overrides=None, all_types=True) -> Problem:
+    rng = np.random.default_rng(seed)
+    graphs = []
+    for gid in range(n_graphs):
+        n = int(rng.integers(n_lo, n_hi + 1))
+        graphs.append(synthetic_graph(rng, n, gid, n_types))
+    enc = NodeFeatureOneHotEncoder(graphs, 'type')
+    mgs = [ModelGraph(g, enc) for g in graphs]
+    ov = dict(flags_overrides or {})
+    if n_max != 10 and 'layer_3' not in ov and ov.get('num_layers', 5) == 5:
+        ov['layer_3'] = 'Padding:max_in_dims={},padding_value=0'.format(n_max)
+        ov['layer_4'] = 'NTN:input_dim={},feature_map_dim=10,inneract=relu,dropout=True,' \
+                        'bias=True'.format(n_max)
+    flags = Flags(**ov)
+    d_in = enc.input_dim()
+    layers = create_layers(flags, d_in)
+    pairs = rng.integers(0, n_graphs, size=(n_pairs, 2)).astype(np.int32)
+    d = rng.integers(0, 8, size=n_pairs)
+    nn = np.array([graphs[i].number_of_nodes() + graphs[j].number_of_nodes() for i, j in pairs])
+    labels = np.exp(-flags.yeta * (2.0 * d / nn) ** 2).astype(np.float32)
+    params = glorot_flat(layers, d_in, seed + 1)
+    # non-zero biases so bias paths are exercised
+    params = params + np.float32(0.05) * rng.standard_normal(params.shape).astype(np.float32)
+    return Problem(flags=flags, graphs=graphs, mgs=mgs, d_in=d_in, n_max=n_max, pairs=pairs,
+                   labels=labels, params=params.astype(np.float32), layers=layers)
+
+
+def run_oracle_step(prob: Problem, seed: int, adam: bool = True):
+    spec = prob.oracle_spec()
+    g1, g2 = prob.oracle_graphs()
+    flat = prob.params.astype(np.float64)
+    res = O.fwd_bwd(spec, flat, g1, g2, prob.labels.astype(np.float64), seed)
+    if adam:
+        st = O.adam_init(flat.size)
+        res.new_params = O.adam_tf_step(flat, res.grad, st, lr=prob.flags.learning_rate)
+    return res
