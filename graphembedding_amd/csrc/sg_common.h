@@ -9,14 +9,16 @@
 
 // ---------------------------------------------------------------------------
 // Counter-based dropout RNG.  Bit-exact twin of oracle/siamese_oracle.py
-// (lowbias32, seed_key, dropout_mask).  Replaces TF's unseeded
+// (sg_mix, seed_key, dropout_mask).  Replaces TF's unseeded
 // floor(keep + U[0,1)) masks of layers.py:332-338 / tf.nn.dropout.
 // ---------------------------------------------------------------------------
-__host__ __device__ __forceinline__ uint32_t sg_lowbias32(uint32_t x) {
+// 24-bit-multiply lowbias32 variant: (x & 0xFFFFFF) * C is one full-rate
+// v_mul_u32_u24 on gfx950.
+__host__ __device__ __forceinline__ uint32_t sg_mix(uint32_t x) {
   x ^= x >> 16;
-  x *= 0x7FEB352Du;
+  x = (x & 0xFFFFFFu) * 0x7FEB35u;
   x ^= x >> 15;
-  x *= 0x846CA68Bu;
+  x = (x & 0xFFFFFFu) * 0x846CA7u;
   x ^= x >> 16;
   return x;
 }
@@ -37,13 +39,13 @@ static inline uint32_t sg_keep_threshold(float keep) {
 }
 
 __device__ __forceinline__ uint32_t sg_pair_key(uint32_t key, uint32_t pair) {
-  return sg_lowbias32(pair ^ key);
+  return sg_mix(pair ^ key);
 }
 
 // One 32-bit hash serves two consecutive elements (e and e^1).
 __device__ __forceinline__ uint32_t sg_hash2(uint32_t pk, uint32_t layer, uint32_t side, uint32_t e) {
   const uint32_t ctr = (layer << 26) | (side << 25) | (e >> 1);
-  return sg_lowbias32(ctr ^ pk);
+  return sg_mix(ctr ^ pk);
 }
 
 __device__ __forceinline__ bool sg_keep(uint32_t pk, uint32_t layer, uint32_t side, uint32_t e,

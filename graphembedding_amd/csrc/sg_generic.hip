@@ -472,7 +472,7 @@ static SgGenLaunch sg_generic_launch(const SgGenPlan &P, int64_t n_pairs, bool b
   const size_t gbytes = bwd ? (size_t)((P.n_params + 1 + 3) & ~3) * 4u : 0u;
   const size_t wbytes = (size_t)P.wave_floats * 4u;
   int nw = 4;
-  while (nw > 1 && gbytes + nw * wbytes > 65536u) --nw;
+  while (nw > 1 && gbytes + nw * wbytes > 81920u) --nw;
   L.waves_per_block = nw;
   L.lds_bytes = gbytes + nw * wbytes;
   int per_cu = (int)(163840u / (L.lds_bytes ? L.lds_bytes : 1u));
@@ -486,7 +486,7 @@ static SgGenLaunch sg_generic_launch(const SgGenPlan &P, int64_t n_pairs, bool b
 
 int sg_generic_lds_ok(const SgGenPlan &P, bool bwd) {
   SgGenLaunch L = sg_generic_launch(P, 1, bwd);
-  return L.lds_bytes <= 65536u;
+  return L.lds_bytes <= 163840u;
 }
 
 int64_t sg_generic_slab_floats(const SgGenPlan &P, int64_t n_pairs) {
@@ -499,7 +499,7 @@ int sg_generic_run(const SgGenPlan &P, bool bwd, const void *recs, int64_t n_pai
                    const float *y_stats, float *s_out, float *slab, int *blocks_out,
                    hipStream_t stream) {
   SgGenLaunch L = sg_generic_launch(P, n_pairs, bwd);
-  if (L.lds_bytes > 65536u) return SG_ERR_UNSUPPORTED;
+  if (L.lds_bytes > 163840u) return SG_ERR_UNSUPPORTED;
   GenArgs A;
   A.recs = (const uint8_t *)recs;
   A.n_pairs = n_pairs;
@@ -510,6 +510,11 @@ int sg_generic_run(const SgGenPlan &P, bool bwd, const void *recs, int64_t n_pai
   A.y_stats = y_stats;
   A.s_out = s_out;
   A.slab = slab;
+  if (L.lds_bytes > 65536u) {
+    hipFuncSetAttribute(bwd ? (const void *)sg_generic_kernel<true>
+                            : (const void *)sg_generic_kernel<false>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
+  }
   if (bwd)
     hipLaunchKernelGGL(sg_generic_kernel<true>, dim3(L.blocks), dim3(64 * L.waves_per_block),
                        L.lds_bytes, stream, P, A);

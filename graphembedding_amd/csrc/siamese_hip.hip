@@ -244,8 +244,13 @@ int64_t sg_workspace_bytes(const sg_model_t *model, int64_t n_pairs) {
   PathChoice c = choose_path(model, true);
   if (c.status != SG_OK) return -1;
   const int64_t C = c.plan.n_params + 1;
-  const int64_t slab = c.fast ? sg_fast_slab_floats(c.plan, n_pairs)
-                              : sg_generic_slab_floats(c.plan, n_pairs);
+  // room for either path (SG_DISABLE_FAST may route a fast-path model to the
+  // generic kernel after the workspace was sized)
+  int64_t slab = sg_generic_slab_floats(c.plan, n_pairs);
+  if (c.fast) {
+    const int64_t f = sg_fast_slab_floats(c.plan, n_pairs);
+    if (f > slab) slab = f;
+  }
   int64_t bytes = (slab + (int64_t)kReduceStrands * C) * 4;
   bytes = (bytes + 255) & ~(int64_t)255;
   const int64_t label_bytes = (256 + 2) * 8;

@@ -25,13 +25,14 @@
 #define H2 16
 #define KNT 10
 
-static inline uint32_t lowbias32(uint32_t x) {
-  x ^= x >> 16; x *= 0x7FEB352Du; x ^= x >> 15; x *= 0x846CA68Bu; x ^= x >> 16;
+static inline uint32_t sg_mix(uint32_t x) {
+  x ^= x >> 16; x = (x & 0xFFFFFFu) * 0x7FEB35u; x ^= x >> 15; x = (x & 0xFFFFFFu) * 0x846CA7u;
+  x ^= x >> 16;
   return x;
 }
 static inline int keep_draw(uint32_t pk, uint32_t layer, uint32_t side, uint32_t e, uint32_t thr) {
   if (thr >= 65536u) return 1;
-  uint32_t h = lowbias32(((layer << 26) | (side << 25) | (e >> 1)) ^ pk);
+  uint32_t h = sg_mix(((layer << 26) | (side << 25) | (e >> 1)) ^ pk);
   uint32_t d = (e & 1u) ? (h >> 16) : (h & 0xFFFFu);
   return d < thr;
 }
@@ -106,7 +107,7 @@ int sgc_fwd_bwd(const uint32_t *recs, int64_t n_pairs, int64_t pair_offset, int 
       const float *adj = (const float *)rec;
       const int32_t *types = (const int32_t *)(rec + 2 * NN);
       const int32_t *nn = (const int32_t *)(rec + 2 * NN + 2 * n_max);
-      const uint32_t pk = lowbias32((uint32_t)(pair_offset + p) ^ key);
+      const uint32_t pk = sg_mix((uint32_t)(pair_offset + p) ^ key);
       for (int s = 0; s < 2; ++s) {
         const int n = nn[s];
         const float *A = adj + s * NN;

@@ -25,13 +25,15 @@ import numpy as np
 _M32 = 0xFFFFFFFF
 
 
-def lowbias32(x):
-    """Chris Wellons' lowbias32 integer mixer on uint64 arrays holding u32."""
+def sg_mix(x):
+    """24-bit-multiply variant of Wellons' lowbias32 mixer (uint64 arrays holding
+    u32): both multiplies take the low 24 bits of x, i.e. the gfx950
+    full-rate v_mul_u32_u24 instruction."""
     x = np.asarray(x, dtype=np.uint64) & _M32
     x ^= x >> np.uint64(16)
-    x = (x * np.uint64(0x7FEB352D)) & _M32
+    x = ((x & np.uint64(0xFFFFFF)) * np.uint64(0x7FEB35)) & _M32
     x ^= x >> np.uint64(15)
-    x = (x * np.uint64(0x846CA68B)) & _M32
+    x = ((x & np.uint64(0xFFFFFF)) * np.uint64(0x846CA7)) & _M32
     x ^= x >> np.uint64(16)
     return x
 
@@ -60,10 +62,10 @@ def dropout_mask(seed: int, pair: int, side: int, layer: int, count: int,
     if keep >= 1.0:
         return np.ones(count, dtype=bool)
     thr = keep_threshold(keep)
-    pk = lowbias32(np.uint64((pair & _M32) ^ seed_key(seed)))
+    pk = sg_mix(np.uint64((pair & _M32) ^ seed_key(seed)))
     e = np.arange(count, dtype=np.uint64)
     ctr = (np.uint64(layer) << np.uint64(26)) | (np.uint64(side) << np.uint64(25)) | (e >> np.uint64(1))
-    h = lowbias32(ctr ^ pk)
+    h = sg_mix(ctr ^ pk)
     draw = (h >> (np.uint64(16) * (e & np.uint64(1)))) & np.uint64(0xFFFF)
     return draw < np.uint64(thr)
 

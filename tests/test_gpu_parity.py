@@ -131,3 +131,23 @@ def test_nmax30_aids10k_shape(gpu):
     np.testing.assert_allclose(s, ref.s, rtol=TOL, atol=TOL)
     model.fwd_bwd(batch, seed=5)
     _check_grad(model.grad.cpu().numpy(), ref.grad_mse)
+
+
+def test_fast_path_matches_generic_path(gpu, monkeypatch):
+    """The fused MFMA kernel and the generic LDS kernel agree on the default
+    stack (dropout on) — the generic path is the on-GPU cross-check."""
+    prob = small_problem(n_graphs=40, n_pairs=2000, seed=17)
+    model, batch = prob.make_gpu_model(device=gpu)
+    assert model.kernel_path == 1, 'default stack must take the fused path'
+    seed = 99
+    s_fast = model.pred_sim_without_act(batch, seed=seed).cpu().numpy()
+    model.fwd_bwd(batch, seed=seed)
+    g_fast = model.grad.cpu().numpy()
+    l_fast = float(model.loss_buf[0].item())
+    monkeypatch.setenv('SG_DISABLE_FAST', '1')
+    s_gen = model.pred_sim_without_act(batch, seed=seed).cpu().numpy()
+    model.fwd_bwd(batch, seed=seed)
+    g_gen = model.grad.cpu().numpy()
+    np.testing.assert_allclose(s_fast, s_gen, rtol=1e-5, atol=1e-5)
+    _check_grad(g_fast, g_gen, tol=2e-5)
+    assert abs(l_fast - float(model.loss_buf[0].item())) <= 1e-5 * max(1.0, abs(l_fast))
