@@ -61,7 +61,6 @@ struct FastArgs {
   float ik0, ik1, ik2, ik4;
   float yeta;
   float inv_batch;
-  int final_act, loss_mode, ntn_mode;
   int d_in, n_params;
   int shared_floats, wave_floats;
   int oW0, ob0, oW1, ob1, oWd, obd, oW, oV, oU, obn;
@@ -71,21 +70,20 @@ template <int D>
 struct FastLds {
   static constexpr int RW = 2 * D * D + 2 * D + 4;  // record words (multiple of 4)
   static constexpr int REC = 0;
-  static constexpr int TILE = REC + RW;               // 2 x 16 x TS1 (D1 / gZ1 tiles)
+  static constexpr int TILE = REC + RW;               // 2 x 16 x TS1 (D1 tiles)
   static constexpr int X = TILE + 2 * 16 * TS1;       // x1[12] | x2[12]
-  static constexpr int PM = X + 32;                   // NTN partial m [6][10]
-  static constexpr int M = PM + 64;                   // m[10]
-  static constexpr int G1 = M + 16;                   // ge1 partials [12][12]
-  static constexpr int G2 = G1 + 144;                 // ge2 partials [12][12]
-  static constexpr int GE = G2 + 144;                 // ge[2][12]
-  static constexpr int GW0 = GE + 32;                 // gW0 accumulator [d_in][32]
-  static int wave_floats(int d_in) { return (GW0 + d_in * FH1 + 3) & ~3; }
+  static int wave_floats(int) { return X + 32; }
   static int shared_floats(int d_in) {
-    return ((d_in * FH1 + 3) & ~3) + 2 * D * FK * 12 + FK * 24;
+    return ((d_in * FH1 + 3) & ~3) + 2 * D * FK * 12 + FK * 24 + 2 * FH1 * FH2;
   }
 };
 
-template <int D, bool BWD>
+// draw of element e from a hash shared by the element pair (e, e^1)
+__device__ __forceinline__ bool keep16(uint32_t h, uint32_t hsh, uint32_t thr) {
+  return ((h >> hsh) & 0xFFFFu) < thr;
+}
+
+template <int D, bool BWD, bool ALIGNED, bool INTENDED>
 __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   using L = FastLds<D>;
@@ -94,6 +92,7 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
   const int tid = threadIdx.x;
   const int l = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
   const int g = l >> 4, j = l & 15;
+  const uint32_t pj = (uint32_t)(j & 1), hsh = pj << 4;  // element parity → hash half
   const int d_in = A.d_in;
   const float *__restrict__ prm = A.params;
 
@@ -101,16 +100,12 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
   float *sWa = sW0 + ((d_in * FH1 + 3) & ~3);  // [a][k][12]: W[a][b][k] at b
   float *sWb = sWa + D * FK * 12;               // [b][k][12]: W[a][b][k] at a
   float *sV = sWb + D * FK * 12;                // [k][24]
+  float *sW1 = sV + FK * 24;                    // W1 [32][16] row-major
+  float *sW1T = sW1 + FH1 * FH2;                // W1ᵀ [16][32]
   float *W = smem + A.shared_floats + wv * A.wave_floats;
   float *sRec = W + L::REC;
   float *sT = W + L::TILE;
   float *sX = W + L::X;
-  float *sPM = W + L::PM;
-  float *sM = W + L::M;
-  float *sG1 = W + L::G1;
-  float *sG2 = W + L::G2;
-  float *sGE = W + L::GE;
-  float *sGW0 = W + L::GW0;
 
   for (int i = tid; i < d_in * FH1; i += blockDim.x) sW0[i] = prm[A.oW0 + i];
   for (int i = tid; i < D * FK * 12; i += blockDim.x) {
@@ -122,44 +117,51 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
     const int k = i / 24, c = i - k * 24;
     sV[i] = c < 2 * D ? prm[A.oV + k * 2 * D + c] : 0.f;
   }
+  for (int i = tid; i < FH1 * FH2; i += blockDim.x) {
+    const float w = prm[A.oW1 + i];
+    sW1[i] = w;
+    sW1T[(i % FH2) * FH1 + i / FH2] = w;
+  }
   for (int i = l; i < 2 * 16 * TS1; i += 64) sT[i] = 0.f;
-  if (BWD)
-    for (int i = l; i < d_in * FH1; i += 64) sGW0[i] = 0.f;
   __syncthreads();
 
   // ---- per-lane constants ----
   float w1b[8], w1t[2][4];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) w1b[q] = prm[A.oW1 + (8 * g + q) * FH2 + j];
+  for (int q = 0; q < 8; ++q) w1b[q] = sW1[(8 * g + q) * FH2 + j];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) w1t[t][q] = prm[A.oW1 + (16 * t + j) * FH2 + 4 * g + q];
-  const float b0v[2] = {prm[A.ob0 + j], prm[A.ob0 + 16 + j]};
+    for (int q = 0; q < 4; ++q) w1t[t][q] = sW1[(16 * t + j) * FH2 + 4 * g + q];
+  const float b0v0 = prm[A.ob0 + j], b0v1 = prm[A.ob0 + 16 + j];
   const float b1v = prm[A.ob1 + j];
   const float wdv = prm[A.oWd + j];
   const float bd = prm[A.obd];
+  // NTN lane role: k = j (valid < FK); rows a = 4r + g, r < 3 (valid < D)
+  const bool kv = j < FK;
+  const int kc = kv ? j : FK - 1;
+  const float Uk = kv ? prm[A.oU + kc] : 0.f;
+  const float bnk = kv ? prm[A.obn + kc] : 0.f;
   float usum = 0.f;
 #pragma unroll
   for (int k = 0; k < FK; ++k) usum += prm[A.oU + k];
-  const bool nl = l < 60;             // NTN lane
-  const int ag = nl ? l / 10 : 0, kk = nl ? l - ag * 10 : 0;
-  const int a0 = ag, a1 = ag + 6;     // own NTN rows (a1 valid if < D)
-  const float Uk = prm[A.oU + kk];
-  const float bnk = prm[A.obn + (l < FK ? l : 0)];
-  const bool ntn_ref = A.ntn_mode == SG_NTN_REFERENCE;
   // A-operand row of this lane: tile row i = j ↔ node ni
   const int ri = j & 3, ni = 4 * ri + (j >> 2);
 
   // ---- accumulators ----
   f4 gw1[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
-  float gb0a[2] = {0.f, 0.f}, gb1a = 0.f, gwda = 0.f, gbda = 0.f;
-  float gWn[2][D];
+  // gW0 = Σ Xᵀ·gZ0 on MFMA: [type tile τ][feature tile t], rows = types 16τ + 4g + r
+  f4 gw0[2][2] = {{f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}},
+                  {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}}};
+  float gb0a0 = 0.f, gb0a1 = 0.f, gb1a = 0.f, gwda = 0.f, gbda = 0.f;
+  float gWn[3][D];
 #pragma unroll
-  for (int b = 0; b < D; ++b) gWn[0][b] = gWn[1][b] = 0.f;
-  float gVa[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int b = 0; b < D; ++b) gWn[r][b] = 0.f;
+  float gVa[3] = {0.f, 0.f, 0.f}, gVb[3] = {0.f, 0.f, 0.f};
   float gbn = 0.f, gUa = 0.f, lossa = 0.f;
-  const float ybar = (BWD && A.loss_mode == SG_LOSS_BROADCAST) ? A.y_stats[0] : 0.f;
+  const float ybar = (BWD && !ALIGNED) ? A.y_stats[0] : 0.f;
 
   const int64_t stride = (int64_t)gridDim.x * nw;
   int64_t p = (int64_t)blockIdx.x * nw + wv;
@@ -190,64 +192,88 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
       }
     }
     const int *ty = (const int *)(sRec + 2 * D * D);
-    const int Nn[2] = {((const int *)sRec)[2 * D * D + 2 * D],
-                       ((const int *)sRec)[2 * D * D + 2 * D + 1]};
-    const float label = sRec[2 * D * D + 2 * D + 2];
+    const int N0 = ((const int *)sRec)[2 * D * D + 2 * D];
+    const int N1 = ((const int *)sRec)[2 * D * D + 2 * D + 1];
     const uint32_t pk = sg_pair_key(A.key, (uint32_t)(A.pair_offset + p));
+
+    // ---- layer-0 (node) and NTN-input dropout masks: one hash per lane, one ballot ----
+    // lane l: side (l>>4)&1, element l&15; lanes <32 layer 0, lanes >=32 layer 4
+    uint64_t kmask;
+    {
+      const int side = (l >> 4) & 1, e = l & 15;
+      const bool hi = l >= 32;
+      const uint32_t h = sg_hash2(pk, hi ? 4u : 0u, (uint32_t)side, (uint32_t)e);
+      const int lim = hi ? D : (side ? N1 : N0);
+      kmask = __ballot((e < lim) & keep16(h, (uint32_t)(e & 1) << 4, hi ? A.thr4 : A.thr0));
+    }
 
     // ================= forward =================
     float af[2][3];
     f4 d1[2][2];
-    f4 zp2[2];            // zpre rows r<3 (r=3 unused)
+    f4 zp2[2];
     f4 d2[2];
-    uint32_t bits[2];     // per instance: r*8 + t*4 + {0:keep0,1:keep1,2:pos1,3:keep2}
+    uint32_t bits[2];   // per instance r*8 + t*4 + {1: keep1, 2: pos1}, r*8 + {4: keep2 (t=1 slot)}
+    f4 p1[2][2];
     int tyr[2][3];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int Ns = Nn[s];
+      const int Ns = s ? N1 : N0;
       const float *As = sRec + s * D * D;
-      const bool rowok = ri < 3 && ni < Ns;
+      const bool rowok = (ri < 3) & (ni < Ns);
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         const int c = 4 * q + g;
-        af[s][q] = (rowok && c < Ns) ? As[ni * D + c] : 0.f;
+        const float v = As[(rowok ? ni : 0) * D + (c < D ? c : 0)];
+        af[s][q] = (rowok & (c < Ns)) ? v : 0.f;
       }
-      uint32_t bs = 0u;
       f4 z0[2];
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         const int n = 4 * r + g;
-        const bool vr = n < Ns;
-        int t_ = vr ? ty[s * D + n] : 0;
+        int t_ = ty[s * D + (n < D ? n : 0)];
         t_ = t_ < 0 ? 0 : (t_ >= d_in ? d_in - 1 : t_);
         tyr[s][r] = t_;
-        const bool k0 = vr && sg_keep(pk, 0, s, n, A.thr0);
-        bs |= (k0 ? 1u : 0u) << (r * 8);
+        const bool k0 = (kmask >> (16 * s + n)) & 1ull;   // 0 for n >= Ns
         z0[0][r] = k0 ? sW0[t_ * FH1 + j] * A.ik0 : 0.f;
         z0[1][r] = k0 ? sW0[t_ * FH1 + 16 + j] * A.ik0 : 0.f;
       }
       z0[0][3] = z0[1][3] = 0.f;
-      // P1 = Â Z0 + b0 ; H1 = relu ; D1 = dropout
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int t = 0; t < 2; ++t) {   // P1 = Â Z0 + b0
+        const float bb = t ? b0v1 : b0v0;
         f4 acc;
 #pragma unroll
-        for (int r = 0; r < 3; ++r) acc[r] = (4 * r + g < Ns) ? b0v[t] : 0.f;
+        for (int r = 0; r < 3; ++r) acc[r] = (4 * r + g < Ns) ? bb : 0.f;
         acc[3] = 0.f;
 #pragma unroll
         for (int q = 0; q < 3; ++q) acc = mfma4(af[s][q], z0[t][q], acc);
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          const int n = 4 * r + g;
-          const bool vr = n < Ns;
-          const float v = acc[r];
-          const bool pos = vr && v > 0.f;
-          const bool k1 = vr && sg_keep(pk, 1, s, n * FH1 + 16 * t + j, A.thr1);
-          d1[s][t][r] = (pos && k1) ? v * A.ik1 : 0.f;
-          bs |= ((k1 ? 2u : 0u) | (pos ? 4u : 0u)) << (r * 8 + t * 4);
-        }
-        d1[s][t][3] = 0.f;
+        p1[s][t] = acc;
       }
+    }
+    // H1 = relu(P1), D1 = dropout(H1): lanes j, j^1 share a hash; even lanes hash
+    // the t = 0 element pair, odd lanes the t = 1 pair, swapped by DPP.
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int Ns = s ? N1 : N0;
+      uint32_t bs = 0u;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int n = 4 * r + g;
+        const uint32_t hm = sg_hash2(pk, 1u, (uint32_t)s,
+                                     (uint32_t)(2 * (n * 16 + 8 * (int)pj + (j >> 1))));
+        const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);
+        const uint32_t h0 = pj ? ho : hm, h1 = pj ? hm : ho;
+        const bool vr = n < Ns;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const float v = p1[s][t][r];
+          const bool pos = vr & (v > 0.f);
+          const bool k1 = vr & keep16(t ? h1 : h0, hsh, A.thr1);
+          d1[s][t][r] = (pos & k1) ? v * A.ik1 : 0.f;
+          bs |= ((k1 ? 1u : 0u) | (pos ? 2u : 0u)) << (r * 8 + t * 4);
+        }
+      }
+      d1[s][0][3] = d1[s][1][3] = 0.f;
       bits[s] = bs;
       float *T = sT + s * 16 * TS1;
 #pragma unroll
@@ -256,10 +282,10 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
         for (int r = 0; r < 4; ++r) T[(4 * g + r) * TS1 + 16 * t + j] = d1[s][t][r];
     }
     sg_wsync();
-    // Z1 = D1 W1 ; H2 = Â Z1 + b1 ; D2 ; zpre = D2 Wd + bd
+    f4 h2[2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int Ns = Nn[s];
+    for (int s = 0; s < 2; ++s) {   // Z1 = D1 W1 ; H2 = Â Z1 + b1
+      const int Ns = s ? N1 : N0;
       const float *T = sT + s * 16 * TS1 + j * TS1 + 8 * g;
       const f4 lo = *(const f4 *)T, hi = *(const f4 *)(T + 4);
       f4 z1 = {0.f, 0.f, 0.f, 0.f};
@@ -267,201 +293,181 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
       for (int q = 0; q < 4; ++q) z1 = mfma4(lo[q], w1b[q], z1);
 #pragma unroll
       for (int q = 0; q < 4; ++q) z1 = mfma4(hi[q], w1b[4 + q], z1);
-      f4 h2;
+      f4 acc;
 #pragma unroll
-      for (int r = 0; r < 3; ++r) h2[r] = (4 * r + g < Ns) ? b1v : 0.f;
-      h2[3] = 0.f;
+      for (int r = 0; r < 3; ++r) acc[r] = (4 * r + g < Ns) ? b1v : 0.f;
+      acc[3] = 0.f;
 #pragma unroll
-      for (int q = 0; q < 3; ++q) h2 = mfma4(af[s][q], z1[q], h2);
+      for (int q = 0; q < 3; ++q) acc = mfma4(af[s][q], z1[q], acc);
+      h2[s] = acc;
+    }
+    // D2 = dropout(H2) (even lanes hash side 0, odd lanes side 1); zpre = D2·Wd + bd;
+    // x = dropout(pad(relu(zpre))): row group g holds x_s[4r+g]
+    float xo[2][3];
 #pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        const int n = 4 * r + g;
-        const bool k2 = n < Ns && sg_keep(pk, 2, s, n * FH2 + j, A.thr2);
-        d2[s][r] = k2 ? h2[r] * A.ik2 : 0.f;
-        bits[s] |= (k2 ? 8u : 0u) << (r * 8);
-        zp2[s][r] = row_sum16(d2[s][r] * wdv) + bd;
+    for (int r = 0; r < 3; ++r) {
+      const int n = 4 * r + g;
+      const uint32_t hm = sg_hash2(pk, 2u, pj, (uint32_t)(2 * (n * 8 + (j >> 1))));
+      const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int Ns = s ? N1 : N0;
+        const uint32_t h = (s == (int)pj) ? hm : ho;
+        const bool k2 = (n < Ns) & keep16(h, hsh, A.thr2);
+        d2[s][r] = k2 ? h2[s][r] * A.ik2 : 0.f;
+        bits[s] |= (k2 ? 4u : 0u) << (r * 8);
+        const float z = row_sum16(d2[s][r] * wdv) + bd;
+        zp2[s][r] = z;
+        const bool k4 = (kmask >> (32 + 16 * s + n)) & 1ull;
+        xo[s][r] = ((n < Ns) & (z > 0.f) & k4) ? z * A.ik4 : 0.f;
       }
-      d2[s][3] = 0.f;
-      // e = relu(zpre) for real nodes, 0-padded to D (Padding, layers.py:223-227);
-      // NTN input dropout (layers.py:287-288)
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        const int n = 4 * r + g;
-        const float e = (n < Ns && zp2[s][r] > 0.f) ? zp2[s][r] : 0.f;
-        if (j == 0 && n < D) sX[s * 12 + n] = sg_keep(pk, 4, s, n, A.thr4) ? e * A.ik4 : 0.f;
+    }
+    // publish x1 | x2 for the lanes that need every element
+    if (j < 3) {
+      const float v0 = j == 0 ? xo[0][0] : (j == 1 ? xo[0][1] : xo[0][2]);
+      const float v1 = j == 0 ? xo[1][0] : (j == 1 ? xo[1][1] : xo[1][2]);
+      const int n = 4 * j + g;
+      if (n < D) {
+        sX[n] = v0;
+        sX[12 + n] = v1;
       }
     }
     sg_wsync();
 
     // ================= NTN head (layers.py:282-310) =================
-    float x1[D], x2[D];
+    float x2[D];
 #pragma unroll
-    for (int b = 0; b < D; ++b) {
-      x1[b] = sX[b];
-      x2[b] = sX[12 + b];
+    for (int b = 0; b < D; ++b) x2[b] = sX[12 + b];
+    float u[3];
+    float mpart = 0.f;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int a = 4 * r + g;
+      const int ac = a < D ? a : 0;
+      const float *wa = sWa + (ac * FK + kc) * 12;
+      float acc = 0.f;
+#pragma unroll
+      for (int b = 0; b < D; ++b) acc = fmaf(wa[b], x2[b], acc);
+      u[r] = acc;
+      // x1[a] u[a][k] + V[k][a] x1[a] + V[k][D+a] x2[a]   (x of invalid a is 0)
+      mpart = fmaf(xo[0][r], acc + sV[kc * 24 + ac], mpart);
+      mpart = fmaf(xo[1][r], sV[kc * 24 + D + ac], mpart);
     }
-    float u0 = 0.f, u1 = 0.f, xv[4] = {0.f, 0.f, 0.f, 0.f}, x1a0 = 0.f, x1a1 = 0.f;
-    if (nl) {
-      const float *wa0 = sWa + (a0 * FK + kk) * 12;
-#pragma unroll
-      for (int b = 0; b < D; ++b) u0 = fmaf(wa0[b], x2[b], u0);
-      x1a0 = sX[a0];
-      float part = x1a0 * u0;
-      if (a1 < D) {
-        const float *wa1 = sWa + (a1 * FK + kk) * 12;
-#pragma unroll
-        for (int b = 0; b < D; ++b) u1 = fmaf(wa1[b], x2[b], u1);
-        x1a1 = sX[a1];
-        part = fmaf(x1a1, u1, part);
-      }
-#pragma unroll
-      for (int ii = 0; ii < 4; ++ii) {
-        const int i = 4 * ag + ii;
-        if (i < 2 * D) {
-          xv[ii] = sX[i < D ? i : 12 + i - D];
-          part = fmaf(sV[kk * 24 + i], xv[ii], part);
-        }
-      }
-      sPM[ag * 10 + kk] = part;
-    }
-    sg_wsync();
-    if (l < FK) {
-      float m = bnk;
-#pragma unroll
-      for (int q = 0; q < 6; ++q) m += sPM[q * 10 + l];
-      sM[l] = m;
-    }
-    sg_wsync();
-    float rsum = 0.f, sdot = 0.f;
-#pragma unroll
-    for (int k = 0; k < FK; ++k) {
-      const float mk = sM[k];
-      const float rk = mk > 0.f ? mk : 0.f;
-      rsum += rk;
-      sdot = fmaf(prm[A.oU + k], rk, sdot);
-    }
-    const float sv = ntn_ref ? usum * rsum : sdot;
+    float m = mpart + __shfl_xor(mpart, 16, 64);
+    m = m + __shfl_xor(m, 32, 64) + bnk;
+    const float rk = (kv & (m > 0.f)) ? m : 0.f;
+    const float rsum = row_sum16(rk);
+    const float sv = INTENDED ? row_sum16(Uk * rk) : usum * rsum;
     if (!BWD) {
       if (l == 0) A.s_out[p] = sv;
       continue;
     }
     if (A.s_out && l == 0) A.s_out[p] = sv;
-    const float yhat = sg_final(A.final_act, A.yeta, sv);
+    const float yhat = expf(-A.yeta * sv * sv);
     float gy;
-    if (A.loss_mode == SG_LOSS_BROADCAST) {
+    if (!ALIGNED) {
       gy = yhat - ybar;
       lossa += 0.5f * gy * gy;
     } else {
-      const float dl = yhat - label;
+      const float dl = yhat - sRec[2 * D * D + 2 * D + 2];
       gy = dl * A.inv_batch;
       lossa += 0.5f * dl * dl * A.inv_batch;
     }
-    const float gs = gy * sg_final_grad(A.final_act, A.yeta, sv, yhat);
+    const float gs = gy * (-2.f * A.yeta * sv * yhat);
 
     // ================= NTN backward =================
-    if (nl) {
-      const float mk = sM[kk];
-      const float gr = ntn_ref ? gs * usum : gs * Uk;
-      const float gmk = mk > 0.f ? gr : 0.f;
-      if (ag == 0) {
-        gbn += gmk;
-        gUa += ntn_ref ? gs * rsum : gs * (mk > 0.f ? mk : 0.f);
-      }
-      const float c0 = gmk * x1a0, c1 = gmk * x1a1;
+    const float gmk = (kv & (m > 0.f)) ? (INTENDED ? gs * Uk : gs * usum) : 0.f;
+    if (g == 0) {
+      gbn += gmk;
+      gUa += INTENDED ? gs * rk : gs * rsum;
+    }
+    float ge[2][3];
+    {
+      float x1[D];
 #pragma unroll
-      for (int b = 0; b < D; ++b) {
-        gWn[0][b] = fmaf(c0, x2[b], gWn[0][b]);
-        gWn[1][b] = fmaf(c1, x2[b], gWn[1][b]);
-      }
+      for (int a = 0; a < D; ++a) x1[a] = sX[a];
 #pragma unroll
-      for (int ii = 0; ii < 4; ++ii) gVa[ii] = fmaf(gmk, xv[ii], gVa[ii]);
-      sG1[a0 * 12 + kk] = gmk * (sV[kk * 24 + a0] + u0);
-      if (a1 < D) sG1[a1 * 12 + kk] = gmk * (sV[kk * 24 + a1] + u1);
-      {
-        const float *wb = sWb + (a0 * FK + kk) * 12;   // b0 = ag
+      for (int r = 0; r < 3; ++r) {
+        const int a = 4 * r + g;
+        const int ac = a < D ? a : 0;
+        const float c = gmk * xo[0][r];
+#pragma unroll
+        for (int b = 0; b < D; ++b) gWn[r][b] = fmaf(c, x2[b], gWn[r][b]);
+        gVa[r] = fmaf(gmk, xo[0][r], gVa[r]);
+        gVb[r] = fmaf(gmk, xo[1][r], gVb[r]);
+        const float t1 = gmk * (sV[kc * 24 + ac] + u[r]);
+        const float *wb = sWb + (ac * FK + kc) * 12;
         float w = 0.f;
 #pragma unroll
-        for (int a = 0; a < D; ++a) w = fmaf(x1[a], wb[a], w);
-        sG2[a0 * 12 + kk] = gmk * (w + sV[kk * 24 + D + a0]);
-      }
-      if (a1 < D) {
-        const float *wb = sWb + (a1 * FK + kk) * 12;   // b1 = ag + 6
-        float w = 0.f;
-#pragma unroll
-        for (int a = 0; a < D; ++a) w = fmaf(x1[a], wb[a], w);
-        sG2[a1 * 12 + kk] = gmk * (w + sV[kk * 24 + D + a1]);
+        for (int aa = 0; aa < D; ++aa) w = fmaf(x1[aa], wb[aa], w);
+        const float t2 = gmk * (sV[kc * 24 + D + ac] + w);
+        const float g1 = row_sum16(t1), g2 = row_sum16(t2);
+        const bool k40 = (kmask >> (32 + a)) & 1ull, k41 = (kmask >> (48 + a)) & 1ull;
+        ge[0][r] = (k40 & (a < D)) ? g1 * A.ik4 : 0.f;
+        ge[1][r] = (k41 & (a < D)) ? g2 * A.ik4 : 0.f;
       }
     }
-    sg_wsync();
-    if (l < 24) {
-      const int s = l / 12, q = l - s * 12;
-      if (q < D) {
-        const float *row = (s ? sG2 : sG1) + q * 12;
-        float gx = 0.f;
-#pragma unroll
-        for (int k = 0; k < FK; ++k) gx += row[k];
-        sGE[s * 12 + q] = sg_keep(pk, 4, s, q, A.thr4) ? gx * A.ik4 : 0.f;
-      }
-    }
-    sg_wsync();
 
     // ================= GCN backward =================
-    f4 gz1[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int Ns = Nn[s];
+      const int Ns = s ? N1 : N0;
       f4 gh2;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         const int n = 4 * r + g;
-        const float ge = n < D ? sGE[s * 12 + n] : 0.f;
-        const float gp = (n < Ns && zp2[s][r] > 0.f) ? ge : 0.f;  // Dense relu'
+        const float gp = ((n < Ns) & (zp2[s][r] > 0.f)) ? ge[s][r] : 0.f;  // Dense relu'
         gwda = fmaf(d2[s][r], gp, gwda);
-        if (j == 0) gbda += gp;
-        const float v = ((bits[s] >> (r * 8)) & 8u) ? gp * wdv * A.ik2 : 0.f;
+        gbda += j == 0 ? gp : 0.f;
+        const float v = ((bits[s] >> (r * 8)) & 4u) ? gp * wdv * A.ik2 : 0.f;
         gb1a += v;
         gh2[r] = v;
       }
       gh2[3] = 0.f;
-      f4 z = {0.f, 0.f, 0.f, 0.f};  // gZ1 = Âᵀ gH2  (Â symmetric, checked at pack time)
+      // gZ1 = Âᵀ gH2 in both orientations (Â symmetric, checked at pack time):
+      //   gz1  rows = nodes (B of gW1 = D1ᵀ gZ1),  gz1t rows = j (A of gD1 = gZ1 W1ᵀ)
+      f4 gz1 = {0.f, 0.f, 0.f, 0.f}, gz1t = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < 3; ++q) z = mfma4(af[s][q], gh2[q], z);
-      gz1[s] = z;
+      for (int q = 0; q < 3; ++q) {
+        gz1 = mfma4(af[s][q], gh2[q], gz1);
+        gz1t = mfma4(gh2[q], af[s][q], gz1t);
+      }
+      const float *T1 = sT + s * 16 * TS1;
 #pragma unroll
-      for (int t = 0; t < 2; ++t)    // gW1 += D1ᵀ gZ1
+      for (int t = 0; t < 2; ++t)    // gW1 += D1ᵀ gZ1 (A operand = this lane's D1 entries)
 #pragma unroll
-        for (int q = 0; q < 3; ++q) gw1[t] = mfma4(d1[s][t][q], z[q], gw1[t]);
-      float *T = sT + s * 16 * TS1;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) T[(4 * g + r) * TS2 + j] = z[r];
-    }
-    sg_wsync();
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int Ns = Nn[s];
-      const f4 ga = *(const f4 *)(sT + s * 16 * TS1 + j * TS2 + 4 * g);
+        for (int q = 0; q < 3; ++q)
+          gw1[t] = mfma4(T1[(4 * g + q) * TS1 + 16 * t + j], gz1[q], gw1[t]);
       const uint32_t bs = bits[s];
+      // one-hot Xᵀ rows for gW0: k-step q ↔ node 4q + g, row i = j ↔ type 16τ + j
+      float xo0[3], xo1[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const bool k0 = (kmask >> (16 * s + 4 * q + g)) & 1ull;
+        xo0[q] = (k0 & (tyr[s][q] == j)) ? A.ik0 : 0.f;
+        xo1[q] = (k0 & (tyr[s][q] == 16 + j)) ? A.ik0 : 0.f;
+      }
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        f4 gd = {0.f, 0.f, 0.f, 0.f};  // gD1 = gZ1 W1ᵀ
+        f4 gd = {0.f, 0.f, 0.f, 0.f};  // gD1 = gZ1 W1ᵀ  (A = gZ1 from gz1t, B = W1[16t+j][4g+q])
 #pragma unroll
-        for (int q = 0; q < 4; ++q) gd = mfma4(ga[q], w1t[t][q], gd);
+        for (int q = 0; q < 4; ++q) gd = mfma4(gz1t[q], w1t[t][q], gd);
         f4 gp1;
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
           const uint32_t b = bs >> (r * 8 + t * 4);
-          const float v = ((b & 6u) == 6u) ? gd[r] * A.ik1 : 0.f;  // keep1 && pos
-          gb0a[t] += v;
-          gp1[r] = v;
+          gp1[r] = ((b & 3u) == 3u) ? gd[r] * A.ik1 : 0.f;  // keep1 && pos
         }
         gp1[3] = 0.f;
+        if (t) gb0a1 += gp1[0] + gp1[1] + gp1[2];
+        else gb0a0 += gp1[0] + gp1[1] + gp1[2];
         f4 gz0 = {0.f, 0.f, 0.f, 0.f};  // gZ0 = Âᵀ gP1
 #pragma unroll
         for (int q = 0; q < 3; ++q) gz0 = mfma4(af[s][q], gp1[q], gz0);
 #pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          if (((bs >> (r * 8)) & 1u) && (4 * r + g) < Ns)
-            atomicAdd(&sGW0[tyr[s][r] * FH1 + 16 * t + j], gz0[r] * A.ik0);
+        for (int q = 0; q < 3; ++q) {  // gW0 += Xᵀ gZ0
+          gw0[0][t] = mfma4(xo0[q], gz0[q], gw0[0][t]);
+          gw0[1][t] = mfma4(xo1[q], gz0[q], gw0[1][t]);
         }
       }
     }
@@ -476,33 +482,40 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
   for (int w = 0; w < nw; ++w) {
     if (wv == w) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) G[A.oW1 + (16 * t + 4 * g + r) * FH2 + j] += gw1[t][r];
-      }
       sg_wsync();
-#pragma unroll
-      for (int t = 0; t < 2; ++t) atomicAdd(&G[A.ob0 + 16 * t + j], gb0a[t]);
+      atomicAdd(&G[A.ob0 + j], gb0a0);
+      atomicAdd(&G[A.ob0 + 16 + j], gb0a1);
       atomicAdd(&G[A.ob1 + j], gb1a);
       atomicAdd(&G[A.oWd + j], gwda);
       atomicAdd(&G[A.obd], gbda);
-      if (nl) {
+      if (kv) {
 #pragma unroll
-        for (int b = 0; b < D; ++b) {
-          G[A.oW + (a0 * D + b) * FK + kk] += gWn[0][b];
-          if (a1 < D) G[A.oW + (a1 * D + b) * FK + kk] += gWn[1][b];
-        }
+        for (int r = 0; r < 3; ++r) {
+          const int a = 4 * r + g;
+          if (a < D) {
 #pragma unroll
-        for (int ii = 0; ii < 4; ++ii) {
-          const int i = 4 * ag + ii;
-          if (i < 2 * D) G[A.oV + kk * 2 * D + i] += gVa[ii];
+            for (int b = 0; b < D; ++b) G[A.oW + (a * D + b) * FK + j] += gWn[r][b];
+            G[A.oV + j * 2 * D + a] += gVa[r];
+            G[A.oV + j * 2 * D + D + a] += gVb[r];
+          }
         }
-        if (ag == 0) {
-          G[A.obn + kk] += gbn;
-          G[A.oU + kk] += gUa;
+        if (g == 0) {
+          G[A.obn + j] += gbn;
+          G[A.oU + j] += gUa;
         }
       }
-      for (int i = l; i < d_in * FH1; i += 64) G[A.oW0 + i] += sGW0[i];
+#pragma unroll
+      for (int tau = 0; tau < 2; ++tau)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int ty_ = 16 * tau + 4 * g + r;
+            if (ty_ < d_in) G[A.oW0 + ty_ * FH1 + 16 * t + j] += gw0[tau][t][r];
+          }
       if (l == 0) G[A.n_params] += lossa;
     }
     __syncthreads();
@@ -570,8 +583,9 @@ static bool fast_shape(const sg_model_t *m, const SgGenPlan &P) {
   if (Ly[4].kind != SG_NTN || Ly[4].input_dim != D || Ly[4].output_dim != FK ||
       Ly[4].act != SG_ACT_RELU || !Ly[4].bias)
     return false;
-  if (m->n_max != D || D > 12 || D < 4) return false;
-  if (m->d_in > 64) return false;
+  if (m->n_max != D || (D != 10 && D != 12)) return false;
+  if (m->final_act != SG_FINAL_GAUSSIAN) return false;
+  if (m->d_in > 32) return false;   // two 16-row type tiles for the one-hot gW0 MFMA
   return P.n_params > 0;
 }
 
@@ -581,17 +595,7 @@ int sg_fast_supported(const sg_model_t *m, const SgGenPlan &P) {
 }
 
 static FastCfg fast_cfg(int D, int d_in, int64_t n_pairs) {
-  switch (D) {
-    case 4: return fast_cfg_t<4>(d_in, n_pairs);
-    case 5: return fast_cfg_t<5>(d_in, n_pairs);
-    case 6: return fast_cfg_t<6>(d_in, n_pairs);
-    case 7: return fast_cfg_t<7>(d_in, n_pairs);
-    case 8: return fast_cfg_t<8>(d_in, n_pairs);
-    case 9: return fast_cfg_t<9>(d_in, n_pairs);
-    case 10: return fast_cfg_t<10>(d_in, n_pairs);
-    case 11: return fast_cfg_t<11>(d_in, n_pairs);
-    default: return fast_cfg_t<12>(d_in, n_pairs);
-  }
+  return D == 12 ? fast_cfg_t<12>(d_in, n_pairs) : fast_cfg_t<10>(d_in, n_pairs);
 }
 
 int64_t sg_fast_slab_floats(const SgGenPlan &P, int64_t n_pairs) {
@@ -599,19 +603,27 @@ int64_t sg_fast_slab_floats(const SgGenPlan &P, int64_t n_pairs) {
   return (int64_t)c.blocks * (P.n_params + 1);
 }
 
+template <int D, bool BWD, bool ALIGNED, bool INTENDED>
+static void launch_one(const FastCfg &c, const FastArgs &A, hipStream_t st) {
+  const void *fn = (const void *)sg_fast_kernel<D, BWD, ALIGNED, INTENDED>;
+  if (c.lds > 65536u)
+    hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds);
+  hipLaunchKernelGGL((sg_fast_kernel<D, BWD, ALIGNED, INTENDED>), dim3(c.blocks),
+                     dim3(64 * c.waves), c.lds, st, A);
+}
+
 template <int D>
-static void launch_fast(const FastCfg &c, bool bwd, const FastArgs &A, hipStream_t st) {
-  if (bwd) {
-    if (c.lds > 65536u)
-      hipFuncSetAttribute((const void *)sg_fast_kernel<D, true>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds);
-    hipLaunchKernelGGL((sg_fast_kernel<D, true>), dim3(c.blocks), dim3(64 * c.waves), c.lds, st, A);
+static void launch_fast(const FastCfg &c, bool bwd, bool aligned, bool intended,
+                        const FastArgs &A, hipStream_t st) {
+  if (!bwd) {
+    if (intended) launch_one<D, false, false, true>(c, A, st);
+    else launch_one<D, false, false, false>(c, A, st);
+  } else if (aligned) {
+    if (intended) launch_one<D, true, true, true>(c, A, st);
+    else launch_one<D, true, true, false>(c, A, st);
   } else {
-    if (c.lds > 65536u)
-      hipFuncSetAttribute((const void *)sg_fast_kernel<D, false>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds);
-    hipLaunchKernelGGL((sg_fast_kernel<D, false>), dim3(c.blocks), dim3(64 * c.waves), c.lds, st,
-                       A);
+    if (intended) launch_one<D, true, false, true>(c, A, st);
+    else launch_one<D, true, false, false>(c, A, st);
   }
 }
 
@@ -643,9 +655,6 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
   A.ik4 = 1.f / k4;
   A.yeta = m->yeta;
   A.inv_batch = batch_total > 0 ? 1.f / (float)batch_total : 0.f;
-  A.final_act = m->final_act;
-  A.loss_mode = m->loss_mode;
-  A.ntn_mode = m->ntn_mode;
   A.d_in = P.d_in;
   A.n_params = P.n_params;
   A.shared_floats = c.shared_floats;
@@ -662,17 +671,10 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
   A.obn = P.offB;
   // the flush reuses the shared weight tables as the slab-row buffer
   if ((size_t)c.shared_floats < (size_t)P.n_params + 1) return SG_ERR_UNSUPPORTED;
-  switch (D) {
-    case 4: launch_fast<4>(c, bwd, A, stream); break;
-    case 5: launch_fast<5>(c, bwd, A, stream); break;
-    case 6: launch_fast<6>(c, bwd, A, stream); break;
-    case 7: launch_fast<7>(c, bwd, A, stream); break;
-    case 8: launch_fast<8>(c, bwd, A, stream); break;
-    case 9: launch_fast<9>(c, bwd, A, stream); break;
-    case 10: launch_fast<10>(c, bwd, A, stream); break;
-    case 11: launch_fast<11>(c, bwd, A, stream); break;
-    default: launch_fast<12>(c, bwd, A, stream); break;
-  }
+  const bool aligned = m->loss_mode == SG_LOSS_ALIGNED;
+  const bool intended = m->ntn_mode == SG_NTN_INTENDED;
+  if (D == 12) launch_fast<12>(c, bwd, aligned, intended, A, stream);
+  else launch_fast<10>(c, bwd, aligned, intended, A, stream);
   if (blocks_out) *blocks_out = c.blocks;
   return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
 }
