@@ -52,7 +52,8 @@ class GraphSet:
 def load_graph_set(name: str = 'syn_aids700nef', n_max: int = 10, seed: int = 123) -> GraphSet:
     tr, te = synthetic_graphs(name, seed)
     graphs = tr + te
-    enc = NodeFeatureOneHotEncoder(graphs, 'type')
+    # sorted (not set-order) columns: identical encoding on every rank (quirk A7)
+    enc = NodeFeatureOneHotEncoder(graphs, 'type').pin_sorted()
     mgs = [ModelGraph(g, enc) for g in graphs]
     store = GraphStore(mgs, n_max, enc.input_dim())
     return GraphSet(graphs=graphs, mgs=mgs, d_in=enc.input_dim(), n_max=n_max, store=store,

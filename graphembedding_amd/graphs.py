@@ -82,12 +82,21 @@ class NodeFeatureOneHotEncoder(object):
     """graphs.py:98-117: the type→column map comes from Python set iteration
     order (quirk A7); it is an explicit, recorded input of the packer."""
 
-    def __init__(self, gs, node_feat_name):
+    def __init__(self, gs, node_feat_name, feat_idx_dic=None):
         self.node_feat_name = node_feat_name
+        if feat_idx_dic is not None:
+            self.feat_idx_dic = dict(feat_idx_dic)
+            return
         inputs_set = set()
         for g in gs:
             inputs_set = inputs_set | set(self._node_feat_dic(g).values())
         self.feat_idx_dic = {feat: idx for idx, feat in enumerate(inputs_set)}
+
+    def pin_sorted(self):
+        """Replace the hash-seed-dependent set order with sorted order, so that
+        every process (rank) encodes identically.  Returns self."""
+        self.feat_idx_dic = {f: i for i, f in enumerate(sorted(self.feat_idx_dic, key=str))}
+        return self
 
     def encode_columns(self, g):
         node_feat_dic = self._node_feat_dic(g)

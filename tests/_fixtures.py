@@ -75,7 +75,7 @@ def small_problem(n_graphs=12, n_pairs=24, seed=5, n_lo=3, n_hi=10, n_max=10, n_
     for gid in range(n_graphs):
         n = int(rng.integers(n_lo, n_hi + 1))
         graphs.append(synthetic_graph(rng, n, gid, n_types))
-    enc = NodeFeatureOneHotEncoder(graphs, 'type')
+    enc = NodeFeatureOneHotEncoder(graphs, 'type').pin_sorted()
     mgs = [ModelGraph(g, enc) for g in graphs]
     ov = dict(flags_overrides or {})
     if n_max != 10 and 'layer_3' not in ov and ov.get('num_layers', 5) == 5:

@@ -1,0 +1,148 @@
+"""Generate golden fixtures by importing the REFERENCE's own (non-TF) modules
+from /root/reference in this container.  Run once; the outputs (.npz/.json) are
+committed and travel to the GPU box — the reference itself never does.
+
+  python tests/golden/make_golden.py
+
+Pinned here (reference modules imported read-only, PYTHONDONTWRITEBYTECODE):
+  model/Siamese/graphs.py     ModelGraph (Â, X COO tuples), NodeFeatureOneHotEncoder
+  model/Siamese/samplers.py   RandomSampler / DistributionSampler pair streams
+  src/similarity.py           GaussianKernel / IdentityKernel, create_sim_kernel
+  src/metrics.py              precision_at_ks, mean_reciprocal_rank, mean_squared_error
+  src/utils.py                sorted_nicely
+Not importable here: TF (absent), src/distance.py and src/results.py (need bs4
+via nx_to_gxl.py) — their logic is restated and tested against these fixtures
+where it feeds them.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = '/root/reference'
+sys.path.insert(0, REF + '/model/Siamese')
+sys.path.insert(0, REF + '/src')
+sys.path.insert(1, ROOT)
+
+import networkx as nx  # noqa: E402
+
+import graphs as ref_graphs  # noqa: E402  (reference)
+import samplers as ref_samplers  # noqa: E402  (reference)
+import similarity as ref_similarity  # noqa: E402  (reference)
+import metrics as ref_metrics  # noqa: E402  (reference)
+import utils as ref_utils  # noqa: E402  (reference)
+
+from graphembedding_amd.data import synthetic_graph  # noqa: E402
+
+
+def graph_set(seed, count, lo, hi):
+    rng = np.random.default_rng(seed)
+    gs = []
+    for gid in range(count):
+        gs.append(synthetic_graph(rng, int(rng.integers(lo, hi + 1)), gid, 29))
+    # one weighted graph and one with a self loop to pin nx.adjacency_matrix semantics
+    g = gs[0].copy()
+    u, v = next(iter(g.edges()))
+    g[u][v]['weight'] = 2.5
+    g.graph['gid'] = count
+    gs.append(g)
+    g2 = gs[1].copy()
+    g2.add_edge('0', '0')
+    g2.graph['gid'] = count + 1
+    gs.append(g2)
+    return gs
+
+
+def gexf_like(g):
+    return {'gid': g.graph['gid'], 'nodes': [[n, g.nodes[n]['type']] for n in g.nodes()],
+            'edges': [[u, v, g[u][v].get('weight', 1.0)] for u, v in g.edges()]}
+
+
+def main():
+    out = {}
+    # ---- F1: preprocessing (graphs.py:34-117) ----
+    gs = graph_set(seed=2024, count=12, lo=1, hi=12)
+    enc = ref_graphs.NodeFeatureOneHotEncoder(gs, 'type')
+    f1 = {'graphs': [gexf_like(g) for g in gs], 'feat_idx_dic': enc.feat_idx_dic,
+          'input_dim': int(enc.input_dim())}
+    arrays = {}
+    for k, g in enumerate(gs):
+        mg = ref_graphs.ModelGraph(g, enc)
+        (xc, xv, xs) = mg.get_node_inputs()
+        (ac, av, ash) = mg.get_laplacians()[0]
+        dense = np.zeros(ash)
+        dense[ac[:, 0], ac[:, 1]] = av
+        arrays['adj_%d' % k] = dense
+        xd = np.zeros(xs)
+        xd[xc[:, 0], xc[:, 1]] = xv
+        arrays['x_%d' % k] = xd
+        arrays['nnz_%d' % k] = np.array(mg.get_node_inputs_num_nonzero())
+    np.savez_compressed(os.path.join(HERE, 'f1_preprocess.npz'), **arrays)
+    with open(os.path.join(HERE, 'f1_preprocess.json'), 'w') as f:
+        json.dump(f1, f, indent=1, sort_keys=True)
+
+    # ---- F2: pair streams (samplers.py:19-68), B + B*B draws per step (A3) ----
+    f2 = {}
+    for n in (52, 420, 7500):
+        items = list(range(n))
+        s = ref_samplers.RandomSampler(items, -1, False)
+        f2['random_%d' % n] = [list(s.get_pair()) for _ in range(2 * n + 37)]
+        f2['random_%d_final_list' % n] = list(s.gs)
+
+    class _G:  # the density sampler reads g.nxgraph
+        def __init__(self, g, i):
+            self.nxgraph = g
+            self.i = i
+    dgs = [_G(g, i) for i, g in enumerate(graph_set(seed=7, count=48, lo=3, hi=12))]
+    for num in (-1, 3):
+        ds = ref_samplers.DistributionSampler(dgs, num, False)
+        f2['density_%d' % num] = [[a.i, b.i] for a, b in (ds.get_pair() for _ in range(40))]
+    with open(os.path.join(HERE, 'f2_samplers.json'), 'w') as f:
+        json.dump(f2, f)
+
+    # ---- F3: similarity kernels (similarity.py:44-76) ----
+    d = np.linspace(0.0, 3.0, 31)
+    f3 = {'d': d.tolist(),
+          'gaussian_0.6': ref_similarity.create_sim_kernel('gaussian', 0.6).dist_to_sim_np(d).tolist(),
+          'gaussian_1.0': ref_similarity.create_sim_kernel('gaussian', 1.0).dist_to_sim_np(d).tolist(),
+          'identity': list(ref_similarity.create_sim_kernel('identity').dist_to_sim_np(d)),
+          'name_0.6': ref_similarity.GaussianKernel(0.6).name(),
+          'shortname_0.6': ref_similarity.GaussianKernel(0.6).shortname(),
+          'name_0.001': ref_similarity.GaussianKernel(0.001).name()}
+    with open(os.path.join(HERE, 'f3_similarity.json'), 'w') as f:
+        json.dump(f3, f)
+
+    # ---- F4: metrics on synthetic result matrices, via duck-typed result objects ----
+    from graphembedding_amd.results import DistanceMatrixResult, SiameseModelResult
+    rng = np.random.default_rng(11)
+    m, n = 6, 25
+    true_d = rng.integers(0, 8, size=(m, n)).astype(float)       # GED-like with ties
+    pred_s = rng.random((m, n))
+    pred_s[:, 3] = pred_s[:, 4]                                    # ties in predictions too
+    true_r = DistanceMatrixResult('syn', 'astar', true_d, true_d * 0.5)
+    pred_r = SiameseModelResult('syn', 'siamese_gcntn_mse', sim_mat=pred_s,
+                                time_mat=rng.random((m, n)))
+    ks = [1, 2, 5, 10, 20]
+    f4 = {'true_dist': true_d.tolist(), 'pred_sim': pred_s.tolist(), 'ks': ks}
+    for norm in (False, True):
+        f4['apk_%s' % norm] = ref_metrics.precision_at_ks(true_r, pred_r, norm, ks).tolist()
+        f4['mrr_%s' % norm] = float(ref_metrics.mean_reciprocal_rank(true_r, pred_r, norm))
+        f4['mse_%s' % norm] = float(ref_metrics.mean_squared_error(true_r, pred_r, 'gaussian', 0.6,
+                                                                   norm))
+    f4['time'] = float(ref_metrics.average_time(pred_r))
+    with open(os.path.join(HERE, 'f4_metrics.json'), 'w') as f:
+        json.dump(f4, f)
+
+    # ---- F5: natural sort (utils.py:148-160) ----
+    names = ['g10.gexf', 'g2.gexf', 'g1.gexf', 'a100', 'a20', 'a3', '7', '11', 'b']
+    with open(os.path.join(HERE, 'f5_utils.json'), 'w') as f:
+        json.dump({'in': names, 'sorted_nicely': ref_utils.sorted_nicely(names)}, f)
+    print('golden fixtures written to', HERE)
+
+
+if __name__ == '__main__':
+    main()

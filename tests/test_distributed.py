@@ -1,0 +1,81 @@
+"""Data-parallel path (graphembedding_amd/shard.py) on CPU with gloo, world 2:
+per-rank pair shards keyed by GLOBAL pair index + one SUM all-reduce of the
+flat gradient reproduce the single-process step.  The per-shard arithmetic is
+the oracle's C restatement standing in for the GPU kernel."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from graphembedding_amd.shard import make_allreduce_hook, shard_range
+
+
+def test_shard_range_partitions():
+    for n in (0, 1, 7, 490000, 1001):
+        for w in (1, 2, 3, 8):
+            spans = [shard_range(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [e - s for s, e in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+class _FakeModel:
+    def __init__(self, grad, loss):
+        self.grad = torch.tensor(grad, dtype=torch.float32)
+        self.loss_buf = torch.tensor([loss, 0.0], dtype=torch.float32)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from _fixtures import small_problem
+        from oracle import cpu_ref
+        prob = small_problem(n_graphs=20, n_pairs=301, seed=31)
+        words = prob.store().pack_host(prob.pairs, prob.labels)
+        ybar = float(prob.labels.astype(np.float64).mean())   # global label stats
+        s0, e0 = shard_range(len(prob.pairs), rank, world)
+        _, g, loss = cpu_ref.fwd_bwd_records(words[s0:e0], prob.n_max, prob.d_in, prob.params,
+                                             77, 0.9, prob.flags.yeta, ybar, pair_offset=s0,
+                                             threads=1)
+        m = _FakeModel(g, loss)
+        make_allreduce_hook()(m)
+        _, g_full, loss_full = cpu_ref.fwd_bwd_records(words, prob.n_max, prob.d_in,
+                                                       prob.params, 77, 0.9, prob.flags.yeta,
+                                                       ybar, threads=1)
+        err = float(np.abs(m.grad.numpy() - g_full).max())
+        lerr = abs(float(m.loss_buf[0]) - loss_full)
+        q.put((rank, err, lerr, float(np.abs(g_full).max())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_step_equals_single_process():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, err, lerr, scale in out:
+        assert err <= 1e-5 * max(1.0, scale), (rank, err)
+        assert lerr <= 1e-4, (rank, lerr)

@@ -1,0 +1,110 @@
+"""Host mirror: flags + layer grammar, packer, feed-dict sampler pattern,
+C restatement vs numpy oracle.  CPU only."""
+import numpy as np
+import pytest
+
+from _fixtures import run_oracle_step, small_problem
+from graphembedding_amd.config import Flags, check_flags
+from graphembedding_amd.layers_factory import create_layers
+from graphembedding_amd.packer import GraphStore, record_words, unpack_host
+from oracle import cpu_ref
+from oracle import siamese_oracle as O
+
+
+def test_default_flags_match_reference_config():
+    f = Flags()
+    assert (f.dataset, f.batch_size, f.yeta, f.dropout, f.weight_decay, f.learning_rate,
+            f.iters, f.num_layers) == ('aids80nef', 5, 0.6, 0.1, 5e-4, 0.01, 20, 5)
+    check_flags(f)
+    layers = create_layers(f, 29)
+    assert [L['kind'] for L in layers] == ['GraphConvolution', 'GraphConvolution', 'Dense',
+                                           'Padding', 'NTN']
+    assert layers == O.default_layers(10, 10) or all(
+        layers[i].get('output_dim') == O.default_layers()[i].get('output_dim') for i in range(3))
+    n = sum(int(np.prod(s)) for _, _, s in O.param_shapes(O.OracleSpec(layers=layers, d_in=29)))
+    assert n == 2725   # 2,725 fp32 params at D_in = 29
+
+
+@pytest.mark.parametrize('spec,msg', [
+    ('Foo:x=1', 'Unknown layer Foo'),
+    ('GraphConvolution:output_dim=32,act=relu', 'must have 3-4 specs'),
+    ('Dense:input_dim=16,output_dim=1,dropout=True,act=relu', 'Dot layer must have 5 specs'),
+    ('Padding:max_in_dims=10', 'Padding layer must have 2 specs'),
+    ('NTN:input_dim=10,feature_map_dim=10,inneract=relu,dropout=Yes,bias=True',
+     'Unknown bool string Yes'),
+    ('Dense:input_dim=16,output_dim=1,dropout=True,act=gelu,bias=True',
+     'Unknown activation function gelu'),
+])
+def test_layer_grammar_errors(spec, msg):
+    f = Flags(layer_2=spec)
+    with pytest.raises(RuntimeError, match=msg):
+        create_layers(f, 29)
+
+
+def test_gcn_input_dim_required_after_first_layer():
+    f = Flags(layer_1='GraphConvolution:output_dim=16,act=identity,dropout=True,bias=True,'
+                      'sparse_inputs=False')
+    with pytest.raises(RuntimeError, match='must be specified'):
+        create_layers(f, 29)
+
+
+def test_packer_record_layout_and_padding():
+    prob = small_problem(n_graphs=6, n_pairs=9, seed=3)
+    store = prob.store()
+    words = store.pack_host(prob.pairs, prob.labels)
+    assert words.shape == (9, record_words(10)) and words.nbytes == 9 * 896
+    f = unpack_host(words, 10)
+    for k, (a, b) in enumerate(prob.pairs):
+        na, nb = prob.mgs[a].num_nodes(), prob.mgs[b].num_nodes()
+        assert tuple(f['n'][k]) == (na, nb)
+        assert np.array_equal(f['adj'][k, 0, :na, :na], prob.mgs[a].adj.astype(np.float32))
+        assert np.all(f['adj'][k, 0, na:, :] == 0) and np.all(f['adj'][k, 1, :, nb:] == 0)
+        assert np.array_equal(f['types'][k, 1, :nb], prob.mgs[b].types)
+        assert f['label'][k] == prob.labels[k] and f['tag'][k] == k
+
+
+def test_packer_rejects_oversize_graph():
+    prob = small_problem(n_graphs=4, n_pairs=2, seed=1, n_lo=11, n_hi=12)
+    with pytest.raises(RuntimeError, match='n_max'):
+        GraphStore(prob.mgs, 10)
+
+
+@pytest.mark.parametrize('dropout', [0.0, 0.1])
+def test_c_restatement_matches_numpy_oracle(dropout):
+    prob = small_problem(n_graphs=16, n_pairs=64, seed=21, flags_overrides=dict(dropout=dropout))
+    ref = run_oracle_step(prob, 1234, adam=False)
+    words = prob.store().pack_host(prob.pairs, prob.labels)
+    ybar = prob.labels.astype(np.float64).mean()
+    s, g, loss = cpu_ref.fwd_bwd_records(words, prob.n_max, prob.d_in, prob.params, 1234,
+                                         1 - dropout, prob.flags.yeta, ybar, threads=2)
+    np.testing.assert_allclose(s, ref.s, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(g, ref.grad_mse, rtol=1e-4, atol=1e-5)
+    label_term = 0.5 * ((prob.labels.astype(np.float64) - ybar) ** 2).sum()
+    assert abs(loss + label_term - ref.loss_mse) < 1e-5 * max(1, ref.loss_mse)
+
+
+def test_feed_dict_sampler_call_pattern():
+    """get_feed_dict draws B input pairs then B×B label pairs (quirk A3): the
+    sampler advances B + B² per train step in 'compat' mode, B in 'aligned'."""
+    from graphembedding_amd.model_mse import SiameseGCNTNMSE
+
+    class FakeData:
+        def __init__(self):
+            self.calls = 0
+            prob = small_problem(n_graphs=8, n_pairs=1, seed=2)
+            self.mgs = prob.mgs
+
+        def get_graph_pair(self, tvt):
+            self.calls += 1
+            return self.mgs[self.calls % 8], self.mgs[(self.calls + 1) % 8]
+
+        def get_dist(self, g1, g2, dc):
+            return 2, 4.0 / (g1.number_of_nodes() + g2.number_of_nodes())
+
+    for mode, expect in (('compat', 5 + 25), ('aligned', 5)):
+        prob = small_problem(n_graphs=8, n_pairs=1, seed=2, flags_overrides=dict(label_stream=mode))
+        model = SiameseGCNTNMSE(prob.d_in, prob.flags, device='cpu', n_max=10, params=prob.params)
+        data = FakeData()
+        batch = model.get_feed_dict(data, None, 'train')
+        assert data.calls == expect and batch.n_pairs == 5
+        assert batch.records.numel() == 5 * record_words(10)
