@@ -121,6 +121,14 @@ def main():
         kern_pairs_s = shard.n / (kern_ms * 1e-3)
         achieved_tf = kern_pairs_s * flops_pair / 1e12
         achieved_gbs = kern_pairs_s * bytes_pair / 1e9
+        traffic = None
+        tj = os.path.join(ROOT, 'profiles', 'traffic.json')
+        if model.kernel_path == 1 and os.path.isfile(tj):
+            with open(tj) as f:
+                t = json.load(f)
+            # HBM bytes per launch from the committed PMC passes of this command
+            # (scripts/gpu_round.sh + scripts/make_profile_summary.py)
+            traffic = t.get('traffic_bytes_per_launch') * shard.n / 490000.0
         cpu = None
         if world == 1 and args.cpu_sample >= 0:
             try:
@@ -148,7 +156,7 @@ def main():
                        'parallelism': 'dp{}'.format(world)},
             'roofline': {'bound': 'mfma', 'achieved': achieved_tf, 'peak': FP32_PEAK_TFLOPS,
                          'unit': 'TFLOP/s', 'frac': achieved_tf / FP32_PEAK_TFLOPS,
-                         'traffic': None,
+                         'traffic': traffic,
                          'note': 'fp32 compute roof (gfx950 vector fp32 == f32 MFMA peak); '
                                  'algorithmic {:.0f} FLOP/pair x {} pairs per launch / sg_fwd_bwd '
                                  'event time {:.3f} ms'.format(flops_pair, shard.n, kern_ms)},
