@@ -74,7 +74,7 @@ struct FastLds {
   static constexpr int X = TILE + 2 * 16 * TS1;       // x1[12] | x2[12]
   static int wave_floats(int) { return X + 32; }
   static int shared_floats(int d_in) {
-    return ((d_in * FH1 + 3) & ~3) + 2 * D * FK * 12 + FK * 24 + 2 * FH1 * FH2;
+    return (d_in + 1) * FH1 + 2 * D * FK * 12 + FK * 24 + 2 * FH1 * FH2;
   }
 };
 
@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
   const float *__restrict__ prm = A.params;
 
   float *sW0 = smem;
-  float *sWa = sW0 + ((d_in * FH1 + 3) & ~3);  // [a][k][12]: W[a][b][k] at b
+  float *sWa = sW0 + (d_in + 1) * FH1;         // [a][k][12]: W[a][b][k] at b
   float *sWb = sWa + D * FK * 12;               // [b][k][12]: W[a][b][k] at a
   float *sV = sWb + D * FK * 12;                // [k][24]
   float *sW1 = sV + FK * 24;                    // W1 [32][16] row-major
@@ -107,7 +107,9 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
   float *sT = W + L::TILE;
   float *sX = W + L::X;
 
-  for (int i = tid; i < d_in * FH1; i += blockDim.x) sW0[i] = prm[A.oW0 + i];
+  // row d_in of the W0 table is zero: the row of a dropped or absent node
+  for (int i = tid; i < (d_in + 1) * FH1; i += blockDim.x)
+    sW0[i] = i < d_in * FH1 ? prm[A.oW0 + i] : 0.f;
   for (int i = tid; i < D * FK * 12; i += blockDim.x) {
     const int x = i / (FK * 12), rem = i - x * FK * 12, k = rem / 12, y = rem - k * 12;
     sWa[i] = y < D ? prm[A.oW + (x * D + y) * FK + k] : 0.f;
@@ -195,29 +197,31 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
     const int N0 = ((const int *)sRec)[2 * D * D + 2 * D];
     const int N1 = ((const int *)sRec)[2 * D * D + 2 * D + 1];
     const uint32_t pk = sg_pair_key(A.key, (uint32_t)(A.pair_offset + p));
+    // wave-uniform: a side with at most 8 nodes has an all-zero third node k-step
+    // (nodes 8..11), skipped in every node-contracting product
+    const bool big0 = __builtin_amdgcn_readfirstlane(N0) > 8;
+    const bool big1 = __builtin_amdgcn_readfirstlane(N1) > 8;
 
     // ---- layer-0 (node) and NTN-input dropout masks: one hash per lane, one ballot ----
-    // lane l: side (l>>4)&1, element l&15; lanes <32 layer 0, lanes >=32 layer 4
+    // lane l: side (l>>4)&1, element l&15; lanes <32 layer 0, lanes >=32 layer 4.
+    // Node validity (e < N_side) is folded into both halves (padded NTN inputs are 0).
     uint64_t kmask;
     {
       const int side = (l >> 4) & 1, e = l & 15;
       const bool hi = l >= 32;
       const uint32_t h = sg_hash2(pk, hi ? 4u : 0u, (uint32_t)side, (uint32_t)e);
-      const int lim = hi ? D : (side ? N1 : N0);
-      kmask = __ballot((e < lim) & keep16(h, (uint32_t)(e & 1) << 4, hi ? A.thr4 : A.thr0));
+      kmask = __ballot((e < (side ? N1 : N0)) &
+                       keep16(h, (uint32_t)(e & 1) << 4, hi ? A.thr4 : A.thr0));
     }
 
     // ================= forward =================
     float af[2][3];
-    f4 d1[2][2];
-    f4 zp2[2];
-    f4 d2[2];
-    uint32_t bits[2];   // per instance r*8 + t*4 + {1: keep1, 2: pos1}, r*8 + {4: keep2 (t=1 slot)}
     f4 p1[2][2];
-    int tyr[2][3];
+    uint32_t tys[2];   // types of rows 4g+r, 6 bits each; 63 = node dropped or absent
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int Ns = s ? N1 : N0;
+      const bool big = s ? big1 : big0;
       const float *As = sRec + s * D * D;
       const bool rowok = (ri < 3) & (ni < Ns);
 #pragma unroll
@@ -227,16 +231,20 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
         af[s][q] = (rowok & (c < Ns)) ? v : 0.f;
       }
       f4 z0[2];
+      uint32_t tp = 0u;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         const int n = 4 * r + g;
         int t_ = ty[s * D + (n < D ? n : 0)];
         t_ = t_ < 0 ? 0 : (t_ >= d_in ? d_in - 1 : t_);
-        tyr[s][r] = t_;
         const bool k0 = (kmask >> (16 * s + n)) & 1ull;   // 0 for n >= Ns
-        z0[0][r] = k0 ? sW0[t_ * FH1 + j] * A.ik0 : 0.f;
-        z0[1][r] = k0 ? sW0[t_ * FH1 + 16 + j] * A.ik0 : 0.f;
+        t_ = k0 ? t_ : 63;
+        tp |= (uint32_t)t_ << (6 * r);
+        const float *w0 = sW0 + (k0 ? t_ : d_in) * FH1 + j;   // row d_in is zero
+        z0[0][r] = w0[0] * A.ik0;
+        z0[1][r] = w0[16] * A.ik0;
       }
+      tys[s] = tp;
       z0[0][3] = z0[1][3] = 0.f;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {   // P1 = Â Z0 + b0
@@ -245,17 +253,19 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
 #pragma unroll
         for (int r = 0; r < 3; ++r) acc[r] = (4 * r + g < Ns) ? bb : 0.f;
         acc[3] = 0.f;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) acc = mfma4(af[s][q], z0[t][q], acc);
+        acc = mfma4(af[s][0], z0[t][0], acc);
+        acc = mfma4(af[s][1], z0[t][1], acc);
+        if (big) acc = mfma4(af[s][2], z0[t][2], acc);
         p1[s][t] = acc;
       }
     }
     // H1 = relu(P1), D1 = dropout(H1): lanes j, j^1 share a hash; even lanes hash
-    // the t = 0 element pair, odd lanes the t = 1 pair, swapped by DPP.
+    // the t = 0 element pair, odd lanes the t = 1 pair, swapped by DPP.  Absent
+    // rows have P1 = 0, so relu zeroes them; the backward reads keep&relu' back
+    // as D1 > 0.
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int Ns = s ? N1 : N0;
-      uint32_t bs = 0u;
+      float *T = sT + s * 16 * TS1;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         const int n = 4 * r + g;
@@ -263,29 +273,20 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
                                      (uint32_t)(2 * (n * 16 + 8 * (int)pj + (j >> 1))));
         const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);
         const uint32_t h0 = pj ? ho : hm, h1 = pj ? hm : ho;
-        const bool vr = n < Ns;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           const float v = p1[s][t][r];
-          const bool pos = vr & (v > 0.f);
-          const bool k1 = vr & keep16(t ? h1 : h0, hsh, A.thr1);
-          d1[s][t][r] = (pos & k1) ? v * A.ik1 : 0.f;
-          bs |= ((k1 ? 1u : 0u) | (pos ? 2u : 0u)) << (r * 8 + t * 4);
+          const bool k1 = keep16(t ? h1 : h0, hsh, A.thr1);
+          T[(4 * g + r) * TS1 + 16 * t + j] = ((v > 0.f) & k1) ? v * A.ik1 : 0.f;
         }
       }
-      d1[s][0][3] = d1[s][1][3] = 0.f;
-      bits[s] = bs;
-      float *T = sT + s * 16 * TS1;
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) T[(4 * g + r) * TS1 + 16 * t + j] = d1[s][t][r];
     }
-    sg_wsync();
+    sg_wsync();   // rows 4g+3 of the tiles stay zero from the prologue
     f4 h2[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {   // Z1 = D1 W1 ; H2 = Â Z1 + b1
       const int Ns = s ? N1 : N0;
+      const bool big = s ? big1 : big0;
       const float *T = sT + s * 16 * TS1 + j * TS1 + 8 * g;
       const f4 lo = *(const f4 *)T, hi = *(const f4 *)(T + 4);
       f4 z1 = {0.f, 0.f, 0.f, 0.f};
@@ -297,13 +298,17 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
 #pragma unroll
       for (int r = 0; r < 3; ++r) acc[r] = (4 * r + g < Ns) ? b1v : 0.f;
       acc[3] = 0.f;
-#pragma unroll
-      for (int q = 0; q < 3; ++q) acc = mfma4(af[s][q], z1[q], acc);
+      acc = mfma4(af[s][0], z1[0], acc);
+      acc = mfma4(af[s][1], z1[1], acc);
+      if (big) acc = mfma4(af[s][2], z1[2], acc);
       h2[s] = acc;
     }
     // D2 = dropout(H2) (even lanes hash side 0, odd lanes side 1); zpre = D2·Wd + bd;
-    // x = dropout(pad(relu(zpre))): row group g holds x_s[4r+g]
-    float xo[2][3];
+    // x = dropout(pad(relu(zpre))): row group g holds x_s[4r+g].  x > 0 exactly when
+    // the node is present, zpre > 0 and the NTN-input element is kept: the backward
+    // uses it as the whole mask of the Dense/Padding/dropout chain.
+    float xo[2][3], d2[2][3];
+    uint32_t kb = 0u;   // layer-2 keep bits, bit 3s + r
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
       const int n = 4 * r + g;
@@ -311,15 +316,13 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
       const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int Ns = s ? N1 : N0;
         const uint32_t h = (s == (int)pj) ? hm : ho;
-        const bool k2 = (n < Ns) & keep16(h, hsh, A.thr2);
+        const bool k2 = keep16(h, hsh, A.thr2);
         d2[s][r] = k2 ? h2[s][r] * A.ik2 : 0.f;
-        bits[s] |= (k2 ? 4u : 0u) << (r * 8);
+        kb |= (k2 ? 1u : 0u) << (3 * s + r);
         const float z = row_sum16(d2[s][r] * wdv) + bd;
-        zp2[s][r] = z;
-        const bool k4 = (kmask >> (32 + 16 * s + n)) & 1ull;
-        xo[s][r] = ((n < Ns) & (z > 0.f) & k4) ? z * A.ik4 : 0.f;
+        const bool k4 = (kmask >> (32 + 16 * s + n)) & 1ull;   // includes n < Ns
+        xo[s][r] = ((z > 0.f) & k4) ? z * A.ik4 : 0.f;
       }
     }
     // publish x1 | x2 for the lanes that need every element
@@ -333,7 +336,6 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
       }
     }
     sg_wsync();
-
     // ================= NTN head (layers.py:282-310) =================
     float x2[D];
 #pragma unroll
@@ -381,7 +383,7 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
       gbn += gmk;
       gUa += INTENDED ? gs * rk : gs * rsum;
     }
-    float ge[2][3];
+    float ge[2][3];   // dL/dx (before the x > 0 mask)
     {
       float x1[D];
 #pragma unroll
@@ -401,25 +403,22 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
 #pragma unroll
         for (int aa = 0; aa < D; ++aa) w = fmaf(x1[aa], wb[aa], w);
         const float t2 = gmk * (sV[kc * 24 + D + ac] + w);
-        const float g1 = row_sum16(t1), g2 = row_sum16(t2);
-        const bool k40 = (kmask >> (32 + a)) & 1ull, k41 = (kmask >> (48 + a)) & 1ull;
-        ge[0][r] = (k40 & (a < D)) ? g1 * A.ik4 : 0.f;
-        ge[1][r] = (k41 & (a < D)) ? g2 * A.ik4 : 0.f;
+        ge[0][r] = row_sum16(t1) * A.ik4;
+        ge[1][r] = row_sum16(t2) * A.ik4;
       }
     }
 
     // ================= GCN backward =================
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int Ns = s ? N1 : N0;
+      const bool big = s ? big1 : big0;
       f4 gh2;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
-        const int n = 4 * r + g;
-        const float gp = ((n < Ns) & (zp2[s][r] > 0.f)) ? ge[s][r] : 0.f;  // Dense relu'
+        const float gp = xo[s][r] > 0.f ? ge[s][r] : 0.f;   // dropout4 · relu' · present
         gwda = fmaf(d2[s][r], gp, gwda);
         gbda += j == 0 ? gp : 0.f;
-        const float v = ((bits[s] >> (r * 8)) & 4u) ? gp * wdv * A.ik2 : 0.f;
+        const float v = ((kb >> (3 * s + r)) & 1u) ? gp * wdv * A.ik2 : 0.f;
         gb1a += v;
         gh2[r] = v;
       }
@@ -427,25 +426,35 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
       // gZ1 = Âᵀ gH2 in both orientations (Â symmetric, checked at pack time):
       //   gz1  rows = nodes (B of gW1 = D1ᵀ gZ1),  gz1t rows = j (A of gD1 = gZ1 W1ᵀ)
       f4 gz1 = {0.f, 0.f, 0.f, 0.f}, gz1t = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        gz1 = mfma4(af[s][q], gh2[q], gz1);
-        gz1t = mfma4(gh2[q], af[s][q], gz1t);
+      gz1 = mfma4(af[s][0], gh2[0], gz1);
+      gz1t = mfma4(gh2[0], af[s][0], gz1t);
+      gz1 = mfma4(af[s][1], gh2[1], gz1);
+      gz1t = mfma4(gh2[1], af[s][1], gz1t);
+      if (big) {
+        gz1 = mfma4(af[s][2], gh2[2], gz1);
+        gz1t = mfma4(gh2[2], af[s][2], gz1t);
       }
-      const float *T1 = sT + s * 16 * TS1;
+      // this lane's D1 entries: A operand of gW1 += D1ᵀ gZ1 and, as D1 > 0, the
+      // keep·relu' mask of gP1
+      const float *T1 = sT + s * 16 * TS1 + 4 * g * TS1 + j;
+      float dq[2][3];
 #pragma unroll
-      for (int t = 0; t < 2; ++t)    // gW1 += D1ᵀ gZ1 (A operand = this lane's D1 entries)
+      for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-          gw1[t] = mfma4(T1[(4 * g + q) * TS1 + 16 * t + j], gz1[q], gw1[t]);
-      const uint32_t bs = bits[s];
+        for (int q = 0; q < 3; ++q) dq[t][q] = T1[q * TS1 + 16 * t];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        gw1[t] = mfma4(dq[t][0], gz1[0], gw1[t]);
+        gw1[t] = mfma4(dq[t][1], gz1[1], gw1[t]);
+        if (big) gw1[t] = mfma4(dq[t][2], gz1[2], gw1[t]);
+      }
       // one-hot Xᵀ rows for gW0: k-step q ↔ node 4q + g, row i = j ↔ type 16τ + j
       float xo0[3], xo1[3];
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
-        const bool k0 = (kmask >> (16 * s + 4 * q + g)) & 1ull;
-        xo0[q] = (k0 & (tyr[s][q] == j)) ? A.ik0 : 0.f;
-        xo1[q] = (k0 & (tyr[s][q] == 16 + j)) ? A.ik0 : 0.f;
+        const int tq = (int)((tys[s] >> (6 * q)) & 63u);
+        xo0[q] = tq == j ? A.ik0 : 0.f;
+        xo1[q] = tq == 16 + j ? A.ik0 : 0.f;
       }
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -454,25 +463,26 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
         for (int q = 0; q < 4; ++q) gd = mfma4(gz1t[q], w1t[t][q], gd);
         f4 gp1;
 #pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          const uint32_t b = bs >> (r * 8 + t * 4);
-          gp1[r] = ((b & 3u) == 3u) ? gd[r] * A.ik1 : 0.f;  // keep1 && pos
-        }
+        for (int r = 0; r < 3; ++r) gp1[r] = dq[t][r] > 0.f ? gd[r] * A.ik1 : 0.f;
         gp1[3] = 0.f;
         if (t) gb0a1 += gp1[0] + gp1[1] + gp1[2];
         else gb0a0 += gp1[0] + gp1[1] + gp1[2];
         f4 gz0 = {0.f, 0.f, 0.f, 0.f};  // gZ0 = Âᵀ gP1
-#pragma unroll
-        for (int q = 0; q < 3; ++q) gz0 = mfma4(af[s][q], gp1[q], gz0);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {  // gW0 += Xᵀ gZ0
-          gw0[0][t] = mfma4(xo0[q], gz0[q], gw0[0][t]);
-          gw0[1][t] = mfma4(xo1[q], gz0[q], gw0[1][t]);
+        gz0 = mfma4(af[s][0], gp1[0], gz0);
+        gz0 = mfma4(af[s][1], gp1[1], gz0);
+        if (big) gz0 = mfma4(af[s][2], gp1[2], gz0);
+        // gW0 += Xᵀ gZ0
+        gw0[0][t] = mfma4(xo0[0], gz0[0], gw0[0][t]);
+        gw0[1][t] = mfma4(xo1[0], gz0[0], gw0[1][t]);
+        gw0[0][t] = mfma4(xo0[1], gz0[1], gw0[0][t]);
+        gw0[1][t] = mfma4(xo1[1], gz0[1], gw0[1][t]);
+        if (big) {
+          gw0[0][t] = mfma4(xo0[2], gz0[2], gw0[0][t]);
+          gw0[1][t] = mfma4(xo1[2], gz0[2], gw0[1][t]);
         }
       }
     }
   }
-
   if (!BWD) return;
   // ---- flush: one wave at a time into the workgroup slab row (deterministic) ----
   __syncthreads();
