@@ -10,7 +10,8 @@ import os
 from typing import List, Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'lib', 'libsiamese_hip.so')
+# SG_LIB overrides the in-tree library (A/B builds of kernel variants)
+LIB_PATH = os.environ.get('SG_LIB') or os.path.join(_HERE, 'lib', 'libsiamese_hip.so')
 
 SG_OK, SG_ERR_ARG, SG_ERR_UNSUPPORTED, SG_ERR_HIP, SG_ERR_SHAPE = 0, 1, 2, 3, 4
 _ERR_NAMES = {1: 'SG_ERR_ARG', 2: 'SG_ERR_UNSUPPORTED', 3: 'SG_ERR_HIP', 4: 'SG_ERR_SHAPE'}

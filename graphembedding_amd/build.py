@@ -22,13 +22,18 @@ def _stale() -> bool:
     return any(os.path.isfile(d) and os.path.getmtime(d) > t for d in deps)
 
 
-def build_hip(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build_hip(force: bool = False, verbose: bool = False, out: str = None, defines=()) -> str:
+    """Build the library in-tree; `out`/`defines` build an A/B variant (e.g. SG_FAST_MAXW=8)."""
+    if out is None and not force and not _stale():
         return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    dst = os.path.abspath(out) if out else OUT
+    os.makedirs(os.path.dirname(dst), exist_ok=True)
     hipcc = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
     cmd = [hipcc, '--offload-arch={}'.format(ARCH), '-O3', '-std=c++17', '-fPIC', '-shared',
-           '-Wall', '-Wno-unused-function', '-Wno-unused-variable', '-o', OUT + '.tmp']
+           # packed f32 VALU (SLP) blocks DPP fusion and stalls beside MFMA
+           '-fno-slp-vectorize',
+           '-Wall', '-Wno-unused-function', '-Wno-unused-variable', '-o', dst + '.tmp']
+    cmd += ['-D' + d for d in defines]
     cmd += [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(' '.join(cmd))
@@ -36,9 +41,13 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError('hipcc failed building libsiamese_hip.so')
-    os.replace(OUT + '.tmp', OUT)
-    return OUT
+    os.replace(dst + '.tmp', dst)
+    return dst
 
 
 if __name__ == '__main__':
-    print(build_hip(force='--force' in sys.argv, verbose=True))
+    # python -m graphembedding_amd.build [--force] [--out PATH] [-DNAME=VAL ...]
+    a = sys.argv[1:]
+    out = a[a.index('--out') + 1] if '--out' in a else None
+    defs = [x[2:] for x in a if x.startswith('-D')]
+    print(build_hip(force='--force' in a, verbose=True, out=out, defines=defs))

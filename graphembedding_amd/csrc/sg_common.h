@@ -42,17 +42,17 @@ __device__ __forceinline__ uint32_t sg_pair_key(uint32_t key, uint32_t pair) {
   return sg_mix(pair ^ key);
 }
 
-// One 32-bit hash serves two consecutive elements (e and e^1).
-__device__ __forceinline__ uint32_t sg_hash2(uint32_t pk, uint32_t layer, uint32_t side, uint32_t e) {
-  const uint32_t ctr = (layer << 26) | (side << 25) | (e >> 1);
-  return sg_mix(ctr ^ pk);
+// One 32-bit hash per (pair, layer, element e of one side's tensor) serves that
+// element of both sides: low 16 bits side 0, high 16 bits side 1 (e < 2^26).
+__device__ __forceinline__ uint32_t sg_hash(uint32_t pk, uint32_t layer, uint32_t e) {
+  return sg_mix(((layer << 26) | e) ^ pk);
 }
 
 __device__ __forceinline__ bool sg_keep(uint32_t pk, uint32_t layer, uint32_t side, uint32_t e,
                                         uint32_t thr) {
   if (thr >= 65536u) return true;
-  const uint32_t h = sg_hash2(pk, layer, side, e);
-  const uint32_t d = (e & 1u) ? (h >> 16) : (h & 0xFFFFu);
+  const uint32_t h = sg_hash(pk, layer, e);
+  const uint32_t d = side ? (h >> 16) : (h & 0xFFFFu);
   return d < thr;
 }
 

@@ -17,6 +17,8 @@
 // Parameter gradients accumulate in registers (gW1 in MFMA accumulators) and a
 // per-wave LDS table (gW0 rows, scattered by node type), flushed once per
 // launch, wave by wave, into one slab row per workgroup (deterministic).
+#include <type_traits>
+
 #include "sg_plan.h"
 
 int sg_num_cus();
@@ -28,16 +30,26 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 constexpr int FH1 = 32, FH2 = 16, FK = 10;
 constexpr int TS1 = 36;  // D1 tile row stride (floats)
 constexpr int TS2 = 20;  // gZ1 tile row stride
+constexpr int W1S = 20;  // W1 table row stride (16 + pad)
+constexpr int W1TS = 36; // W1ᵀ table row stride (32 + pad)
+#ifndef SG_FAST_MAXW
+#define SG_FAST_MAXW 8
+#endif
+// waves per block: 8 = 2 waves per SIMD at up to 256 VGPRs per lane
+constexpr int MAXW = SG_FAST_MAXW;
 
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// DPP lane move with bound_ctrl (no "old" operand to materialise), so the
+// compiler can fold it into the consuming VALU op (v_add_f32_dpp).
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
-                                                               0xF, 0xF, false));
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL,
+                                                            0xF, 0xF, true));
 }
+
 
 // Sum over the 16 lanes of a DPP row; result in every lane of the row.
 __device__ __forceinline__ float row_sum16(float v) {
@@ -71,45 +83,46 @@ struct FastLds {
   static constexpr int RW = 2 * D * D + 2 * D + 4;  // record words (multiple of 4)
   static constexpr int REC = 0;
   static constexpr int TILE = REC + RW;               // 2 x 16 x TS1 (D1 tiles)
-  static constexpr int X = TILE + 2 * 16 * TS1;       // x1[12] | x2[12]
-  static int wave_floats(int) { return X + 32; }
+  static constexpr int X = TILE + 2 * 16 * TS1;       // x1[12] | x2[12] | spare; [47] = 0
+  static int wave_floats(int) { return X + 48; }
   static int shared_floats(int d_in) {
-    return (d_in + 1) * FH1 + 2 * D * FK * 12 + FK * 24 + 2 * FH1 * FH2;
+    return (d_in + 1) * FH1 + 2 * D * FK * 12 + FK * 24 + FH1 * W1S + FH2 * W1TS;
   }
 };
 
-// draw of element e from a hash shared by the element pair (e, e^1)
-__device__ __forceinline__ bool keep16(uint32_t h, uint32_t hsh, uint32_t thr) {
-  return ((h >> hsh) & 0xFFFFu) < thr;
-}
 
 template <int D, bool BWD, bool ALIGNED, bool INTENDED>
-__global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
+__global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   using L = FastLds<D>;
   constexpr int RW4 = L::RW / 4;
   constexpr int NREC = (RW4 + 63) / 64;
   const int tid = threadIdx.x;
-  const int l = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
+  const int l = tid & 63, nw = blockDim.x >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: pair index in SGPRs
   const int g = l >> 4, j = l & 15;
-  const uint32_t pj = (uint32_t)(j & 1), hsh = pj << 4;  // element parity → hash half
+  // dropout hash inputs pk ^ (layer << 26 | e): e = this lane's element index splits
+  // into a uniform part (r, t) and these per-lane parts (disjoint bit fields)
+  const uint32_t lb1 = (uint32_t)(FH1 * g + j);   // layer 1: e = 32 n + f, n = 4r+g, f = 16t+j
+  const uint32_t lb2 = (uint32_t)(FH2 * g + j);   // layer 2: e = 16 n + j
   const int d_in = A.d_in;
   const float *__restrict__ prm = A.params;
 
-  float *sW0 = smem;
-  float *sWa = sW0 + (d_in + 1) * FH1;         // [a][k][12]: W[a][b][k] at b
+  float *sW0 = smem;                            // W0 · ik0, row d_in zero
+  float *sWa = sW0 + (d_in + 1) * FH1;          // [a][k][12]: W[a][b][k] at b
   float *sWb = sWa + D * FK * 12;               // [b][k][12]: W[a][b][k] at a
   float *sV = sWb + D * FK * 12;                // [k][24]
-  float *sW1 = sV + FK * 24;                    // W1 [32][16] row-major
-  float *sW1T = sW1 + FH1 * FH2;                // W1ᵀ [16][32]
+  float *sW1 = sV + FK * 24;                    // W1 · ik1 [32][16], row stride W1S (gD1)
+  float *sW1T = sW1 + FH1 * W1S;                // W1ᵀ [16][32], row stride W1TS (Z1)
   float *W = smem + A.shared_floats + wv * A.wave_floats;
   float *sRec = W + L::REC;
   float *sT = W + L::TILE;
   float *sX = W + L::X;
 
-  // row d_in of the W0 table is zero: the row of a dropped or absent node
+  // Dropout scales are folded into the tables that feed the dropped tensors:
+  // Z0 = (W0 · ik0)[type] and gP1 = keep·relu' · (gZ1 (W1 · ik1)ᵀ).
   for (int i = tid; i < (d_in + 1) * FH1; i += blockDim.x)
-    sW0[i] = i < d_in * FH1 ? prm[A.oW0 + i] : 0.f;
+    sW0[i] = i < d_in * FH1 ? prm[A.oW0 + i] * A.ik0 : 0.f;
   for (int i = tid; i < D * FK * 12; i += blockDim.x) {
     const int x = i / (FK * 12), rem = i - x * FK * 12, k = rem / 12, y = rem - k * 12;
     sWa[i] = y < D ? prm[A.oW + (x * D + y) * FK + k] : 0.f;
@@ -121,20 +134,18 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
   }
   for (int i = tid; i < FH1 * FH2; i += blockDim.x) {
     const float w = prm[A.oW1 + i];
-    sW1[i] = w;
-    sW1T[(i % FH2) * FH1 + i / FH2] = w;
+    sW1[(i / FH2) * W1S + i % FH2] = w * A.ik1;
+    sW1T[(i % FH2) * W1TS + i / FH2] = w;
   }
   for (int i = l; i < 2 * 16 * TS1; i += 64) sT[i] = 0.f;
+  if (l < 48) sX[l] = 0.f;
   __syncthreads();
 
   // ---- per-lane constants ----
-  float w1b[8], w1t[2][4];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) w1b[q] = sW1[(8 * g + q) * FH2 + j];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) w1t[t][q] = sW1[(16 * t + j) * FH2 + 4 * g + q];
+  // MFMA B fragments of W1 read from LDS at use: W1[8g+q][j] (Z1 = D1 W1) and
+  // ik1 · W1[16t+j][4g+q] (gD1 = gZ1 W1ᵀ), contiguous in their tables
+  const float *w1bp = sW1T + j * W1TS + 8 * g;
+  const float *w1tp = sW1 + j * W1S + 4 * g;
   const float b0v0 = prm[A.ob0 + j], b0v1 = prm[A.ob0 + 16 + j];
   const float b1v = prm[A.ob1 + j];
   const float wdv = prm[A.oWd + j];
@@ -147,12 +158,26 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
   float usum = 0.f;
 #pragma unroll
   for (int k = 0; k < FK; ++k) usum += prm[A.oU + k];
-  // A-operand row of this lane: tile row i = j ↔ node ni
+  // A-operand row of this lane: tile row i = j ↔ node ni.  Â is read at static
+  // per-lane offsets; entries outside the n_max × n_max block (tile rows and
+  // columns past n_max) read the always-zero sX[47].  Entries of absent nodes
+  // inside the block are zero by the record contract (siamese_hip.h).
   const int ri = j & 3, ni = 4 * ri + (j >> 2);
+  int afo[2][3];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int c = 4 * q + g;
+      afo[s][q] = (ri < 3 && ni < D && c < D) ? L::REC + s * D * D + ni * D + c : L::X + 47;
+    }
+  int tyo[3];   // record word of the type of node 4r + g (side 0; side 1 at + D)
+#pragma unroll
+  for (int r = 0; r < 3; ++r) tyo[r] = 2 * D * D + (4 * r + g < D ? 4 * r + g : 0);
 
   // ---- accumulators ----
   f4 gw1[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
-  // gW0 = Σ Xᵀ·gZ0 on MFMA: [type tile τ][feature tile t], rows = types 16τ + 4g + r
+  // gW0 / ik0 = Σ Xᵀ·gZ0 on MFMA: [type tile τ][feature tile t], rows = types 16τ + 4g + r
   f4 gw0[2][2] = {{f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}},
                   {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}}};
   float gb0a0 = 0.f, gb0a1 = 0.f, gb1a = 0.f, gwda = 0.f, gbda = 0.f;
@@ -193,296 +218,303 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
           pre[c] = ((const uint4 *)(A.recs + (size_t)pn * (L::RW * 4)))[w4];
       }
     }
-    const int *ty = (const int *)(sRec + 2 * D * D);
-    const int N0 = ((const int *)sRec)[2 * D * D + 2 * D];
-    const int N1 = ((const int *)sRec)[2 * D * D + 2 * D + 1];
+    const int *ty = (const int *)sRec;
+    // wave-uniform node counts (clamped to n_max)
+    int N0 = __builtin_amdgcn_readfirstlane(((const int *)sRec)[2 * D * D + 2 * D]);
+    int N1 = __builtin_amdgcn_readfirstlane(((const int *)sRec)[2 * D * D + 2 * D + 1]);
+    N0 = N0 < 0 ? 0 : (N0 > D ? D : N0);
+    N1 = N1 < 0 ? 0 : (N1 > D ? D : N1);
     const uint32_t pk = sg_pair_key(A.key, (uint32_t)(A.pair_offset + p));
-    // wave-uniform: a side with at most 8 nodes has an all-zero third node k-step
-    // (nodes 8..11), skipped in every node-contracting product
-    const bool big0 = __builtin_amdgcn_readfirstlane(N0) > 8;
-    const bool big1 = __builtin_amdgcn_readfirstlane(N1) > 8;
 
-    // ---- layer-0 (node) and NTN-input dropout masks: one hash per lane, one ballot ----
-    // lane l: side (l>>4)&1, element l&15; lanes <32 layer 0, lanes >=32 layer 4.
-    // Node validity (e < N_side) is folded into both halves (padded NTN inputs are 0).
-    uint64_t kmask;
+    // ---- layer-0 (node) and NTN-input dropout masks: one hash per lane, two ballots ----
+    // lanes 0..15: layer 0, node e = l; lanes 16..31: layer 4, element e = l - 16.
+    // Node presence (e < N_side) is folded in (padded NTN inputs are 0).
+    uint32_t km, km4;   // this lane's view: bit 16s + 4r ↔ node / element 4r + g of side s
     {
-      const int side = (l >> 4) & 1, e = l & 15;
-      const bool hi = l >= 32;
-      const uint32_t h = sg_hash2(pk, hi ? 4u : 0u, (uint32_t)side, (uint32_t)e);
-      kmask = __ballot((e < (side ? N1 : N0)) &
-                       keep16(h, (uint32_t)(e & 1) << 4, hi ? A.thr4 : A.thr0));
+      const int e = l & 15;
+      const bool hi = l >= 16;
+      const uint32_t h = sg_hash(pk, hi ? 4u : 0u, (uint32_t)e);
+      const uint32_t thr = hi ? A.thr4 : A.thr0;
+      const uint64_t b0 = __ballot((l < 32) & (e < N0) & ((h & 0xFFFFu) < thr));
+      const uint64_t b1 = __ballot((l < 32) & (e < N1) & ((h >> 16) < thr));
+      const uint32_t m0 = (uint32_t)(b0 & 0xFFFFu) | ((uint32_t)(b1 & 0xFFFFu) << 16);
+      const uint32_t m4 = (uint32_t)((b0 >> 16) & 0xFFFFu) | ((uint32_t)b1 & 0xFFFF0000u);
+      km = m0 >> g;
+      km4 = m4 >> g;
     }
 
-    // ================= forward =================
-    float af[2][3];
-    f4 p1[2][2];
-    uint32_t tys[2];   // types of rows 4g+r, 6 bits each; 63 = node dropped or absent
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int Ns = s ? N1 : N0;
-      const bool big = s ? big1 : big0;
-      const float *As = sRec + s * D * D;
-      const bool rowok = (ri < 3) & (ni < Ns);
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int c = 4 * q + g;
-        const float v = As[(rowok ? ni : 0) * D + (c < D ? c : 0)];
-        af[s][q] = (rowok & (c < Ns)) ? v : 0.f;
-      }
-      f4 z0[2];
-      uint32_t tp = 0u;
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        const int n = 4 * r + g;
-        int t_ = ty[s * D + (n < D ? n : 0)];
-        t_ = t_ < 0 ? 0 : (t_ >= d_in ? d_in - 1 : t_);
-        const bool k0 = (kmask >> (16 * s + n)) & 1ull;   // 0 for n >= Ns
-        t_ = k0 ? t_ : 63;
-        tp |= (uint32_t)t_ << (6 * r);
-        const float *w0 = sW0 + (k0 ? t_ : d_in) * FH1 + j;   // row d_in is zero
-        z0[0][r] = w0[0] * A.ik0;
-        z0[1][r] = w0[16] * A.ik0;
-      }
-      tys[s] = tp;
-      z0[0][3] = z0[1][3] = 0.f;
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {   // P1 = Â Z0 + b0
-        const float bb = t ? b0v1 : b0v0;
-        f4 acc;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) acc[r] = (4 * r + g < Ns) ? bb : 0.f;
-        acc[3] = 0.f;
-        acc = mfma4(af[s][0], z0[t][0], acc);
-        acc = mfma4(af[s][1], z0[t][1], acc);
-        if (big) acc = mfma4(af[s][2], z0[t][2], acc);
-        p1[s][t] = acc;
-      }
-    }
-    // H1 = relu(P1), D1 = dropout(H1): lanes j, j^1 share a hash; even lanes hash
-    // the t = 0 element pair, odd lanes the t = 1 pair, swapped by DPP.  Absent
-    // rows have P1 = 0, so relu zeroes them; the backward reads keep&relu' back
-    // as D1 > 0.
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      float *T = sT + s * 16 * TS1;
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        const int n = 4 * r + g;
-        const uint32_t hm = sg_hash2(pk, 1u, (uint32_t)s,
-                                     (uint32_t)(2 * (n * 16 + 8 * (int)pj + (j >> 1))));
-        const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);
-        const uint32_t h0 = pj ? ho : hm, h1 = pj ? hm : ho;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const float v = p1[s][t][r];
-          const bool k1 = keep16(t ? h1 : h0, hsh, A.thr1);
-          T[(4 * g + r) * TS1 + 16 * t + j] = ((v > 0.f) & k1) ? v * A.ik1 : 0.f;
-        }
-      }
-    }
-    sg_wsync();   // rows 4g+3 of the tiles stay zero from the prologue
-    f4 h2[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {   // Z1 = D1 W1 ; H2 = Â Z1 + b1
-      const int Ns = s ? N1 : N0;
-      const bool big = s ? big1 : big0;
-      const float *T = sT + s * 16 * TS1 + j * TS1 + 8 * g;
-      const f4 lo = *(const f4 *)T, hi = *(const f4 *)(T + 4);
-      f4 z1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) z1 = mfma4(lo[q], w1b[q], z1);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) z1 = mfma4(hi[q], w1b[4 + q], z1);
-      f4 acc;
-#pragma unroll
-      for (int r = 0; r < 3; ++r) acc[r] = (4 * r + g < Ns) ? b1v : 0.f;
-      acc[3] = 0.f;
-      acc = mfma4(af[s][0], z1[0], acc);
-      acc = mfma4(af[s][1], z1[1], acc);
-      if (big) acc = mfma4(af[s][2], z1[2], acc);
-      h2[s] = acc;
-    }
-    // D2 = dropout(H2) (even lanes hash side 0, odd lanes side 1); zpre = D2·Wd + bd;
-    // x = dropout(pad(relu(zpre))): row group g holds x_s[4r+g].  x > 0 exactly when
-    // the node is present, zpre > 0 and the NTN-input element is kept: the backward
-    // uses it as the whole mask of the Dense/Padding/dropout chain.
-    float xo[2][3], d2[2][3];
-    uint32_t kb = 0u;   // layer-2 keep bits, bit 3s + r
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const int n = 4 * r + g;
-      const uint32_t hm = sg_hash2(pk, 2u, pj, (uint32_t)(2 * (n * 8 + (j >> 1))));
-      const uint32_t ho = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hm, 0xB1, 0xF, 0xF, false);
+    // Pair body for K0 / K1 node k-steps per side: a side with at most 8 nodes
+    // has an all-zero third k-step (nodes 8..11), dropped from every
+    // node-contracting product.  Four straight-line instantiations.
+    auto body = [&](auto K0c, auto K1c) __attribute__((always_inline)) {
+      constexpr int K0 = decltype(K0c)::value, K1 = decltype(K1c)::value;
+      // ================= forward =================
+      float af[2][3];
+      f4 p1[2][2];
+      uint32_t tys[2];   // types of rows 4g+r, 6 bits each; 63 = node dropped or absent
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const uint32_t h = (s == (int)pj) ? hm : ho;
-        const bool k2 = keep16(h, hsh, A.thr2);
-        d2[s][r] = k2 ? h2[s][r] * A.ik2 : 0.f;
-        kb |= (k2 ? 1u : 0u) << (3 * s + r);
-        const float z = row_sum16(d2[s][r] * wdv) + bd;
-        const bool k4 = (kmask >> (32 + 16 * s + n)) & 1ull;   // includes n < Ns
-        xo[s][r] = ((z > 0.f) & k4) ? z * A.ik4 : 0.f;
+        const int KS = s ? K1 : K0;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) af[s][q] = q < KS ? W[afo[s][q]] : 0.f;
+        f4 z0[2];
+        uint32_t tp = 0u;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          if (r < KS) {
+            uint32_t t_ = (uint32_t)ty[tyo[r] + s * D];
+            t_ = min(t_, (uint32_t)(d_in - 1));
+            const uint32_t k0 = (km >> (16 * s + 4 * r)) & 1u;   // 0 for absent nodes
+            const uint32_t tk = k0 ? t_ : 63u;
+            tp |= tk << (6 * r);
+            const float *w0 = sW0 + (k0 ? t_ : (uint32_t)d_in) * FH1 + j;
+            z0[0][r] = w0[0];
+            z0[1][r] = w0[16];
+          } else {
+            tp |= 63u << (6 * r);
+            z0[0][r] = z0[1][r] = 0.f;
+          }
+        }
+        tys[s] = tp;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {   // P1 = Â Z0 + b0  (rows of absent nodes: b0, never read)
+          const float bb = t ? b0v1 : b0v0;
+          f4 acc = {bb, bb, bb, bb};
+#pragma unroll
+          for (int q = 0; q < KS; ++q) acc = mfma4(af[s][q], z0[t][q], acc);
+          p1[s][t] = acc;
+        }
       }
-    }
-    // publish x1 | x2 for the lanes that need every element
-    if (j < 3) {
-      const float v0 = j == 0 ? xo[0][0] : (j == 1 ? xo[0][1] : xo[0][2]);
-      const float v1 = j == 0 ? xo[1][0] : (j == 1 ? xo[1][1] : xo[1][2]);
-      const int n = 4 * j + g;
-      if (n < D) {
-        sX[n] = v0;
-        sX[12 + n] = v1;
+      // H1 = relu(P1), D1 = dropout(H1): one hash per element (node 4r+g, feature
+      // 16t+j) gives both sides' draws.  The backward reads keep·relu' back as D1 > 0.
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          if (r < K0 || r < K1) {
+            const uint32_t h = sg_mix((pk ^ ((1u << 26) | (uint32_t)(128 * r + 16 * t))) ^ lb1);
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              float *T = sT + s * 16 * TS1 + (4 * g + r) * TS1 + 16 * t + j;
+              if (r < (s ? K1 : K0)) {
+                const uint32_t d = s ? (h >> 16) : (h & 0xFFFFu);
+                const float v = fmaxf(p1[s][t][r] * A.ik1, 0.f);
+                *T = d < A.thr1 ? v : 0.f;
+              } else {
+                *T = 0.f;
+              }
+            }
+          } else {
+            sT[(4 * g + r) * TS1 + 16 * t + j] = 0.f;
+            sT[16 * TS1 + (4 * g + r) * TS1 + 16 * t + j] = 0.f;
+          }
+        }
       }
-    }
-    sg_wsync();
-    // ================= NTN head (layers.py:282-310) =================
-    float x2[D];
+      sg_wsync();   // rows 4g+3 of the tiles stay zero from the prologue
+      f4 h2[2];
 #pragma unroll
-    for (int b = 0; b < D; ++b) x2[b] = sX[12 + b];
-    float u[3];
-    float mpart = 0.f;
+      for (int s = 0; s < 2; ++s) {   // Z1 = D1 W1 ; H2 = Â Z1 + b1
+        const int KS = s ? K1 : K0;
+        const float *T = sT + s * 16 * TS1 + j * TS1 + 8 * g;
+        const f4 lo = *(const f4 *)T, hi = *(const f4 *)(T + 4);
+        const f4 wlo = *(const f4 *)w1bp, whi = *(const f4 *)(w1bp + 4);
+        f4 z1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const int a = 4 * r + g;
-      const int ac = a < D ? a : 0;
-      const float *wa = sWa + (ac * FK + kc) * 12;
-      float acc = 0.f;
+        for (int q = 0; q < 4; ++q) z1 = mfma4(lo[q], wlo[q], z1);
 #pragma unroll
-      for (int b = 0; b < D; ++b) acc = fmaf(wa[b], x2[b], acc);
-      u[r] = acc;
-      // x1[a] u[a][k] + V[k][a] x1[a] + V[k][D+a] x2[a]   (x of invalid a is 0)
-      mpart = fmaf(xo[0][r], acc + sV[kc * 24 + ac], mpart);
-      mpart = fmaf(xo[1][r], sV[kc * 24 + D + ac], mpart);
-    }
-    float m = mpart + __shfl_xor(mpart, 16, 64);
-    m = m + __shfl_xor(m, 32, 64) + bnk;
-    const float rk = (kv & (m > 0.f)) ? m : 0.f;
-    const float rsum = row_sum16(rk);
-    const float sv = INTENDED ? row_sum16(Uk * rk) : usum * rsum;
-    if (!BWD) {
-      if (l == 0) A.s_out[p] = sv;
-      continue;
-    }
-    if (A.s_out && l == 0) A.s_out[p] = sv;
-    const float yhat = expf(-A.yeta * sv * sv);
-    float gy;
-    if (!ALIGNED) {
-      gy = yhat - ybar;
-      lossa += 0.5f * gy * gy;
-    } else {
-      const float dl = yhat - sRec[2 * D * D + 2 * D + 2];
-      gy = dl * A.inv_batch;
-      lossa += 0.5f * dl * dl * A.inv_batch;
-    }
-    const float gs = gy * (-2.f * A.yeta * sv * yhat);
+        for (int q = 0; q < 4; ++q) z1 = mfma4(hi[q], whi[q], z1);
+        f4 acc = {b1v, b1v, b1v, b1v};
+#pragma unroll
+        for (int q = 0; q < KS; ++q) acc = mfma4(af[s][q], z1[q], acc);
+        h2[s] = acc;
+      }
+      // D2 = dropout(H2) (one hash per element, both sides); zpre = D2·Wd + bd;
+      // x = dropout(pad(relu(zpre))): row group g holds x_s[4r+g].  x > 0 exactly when
+      // the node is present, zpre > 0 and the NTN-input element is kept: the backward
+      // uses it as the whole mask of the Dense/Padding/dropout chain.
+      float xo[2][3], d2[2][3];
+      uint32_t kb = 0u;   // layer-2 keep bits, bit 3s + r
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        if (r < K0 || r < K1) {
+          const uint32_t h = sg_mix((pk ^ ((2u << 26) | (uint32_t)(64 * r))) ^ lb2);
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            if (r < (s ? K1 : K0)) {
+              const bool k2 = (s ? (h >> 16) : (h & 0xFFFFu)) < A.thr2;
+              d2[s][r] = k2 ? h2[s][r] * A.ik2 : 0.f;
+              kb |= (k2 ? 1u : 0u) << (3 * s + r);
+              const float z = row_sum16(d2[s][r] * wdv) + bd;
+              const bool k4 = (km4 >> (16 * s + 4 * r)) & 1u;   // includes n < Ns
+              xo[s][r] = ((z > 0.f) & k4) ? z * A.ik4 : 0.f;
+            } else {
+              d2[s][r] = 0.f;
+              xo[s][r] = 0.f;
+            }
+          }
+        } else {
+          d2[0][r] = d2[1][r] = xo[0][r] = xo[1][r] = 0.f;
+        }
+      }
+      // publish x1 | x2 for the lanes that need every element
+      if (j < 3) {
+        const float v0 = j == 0 ? xo[0][0] : (j == 1 ? xo[0][1] : xo[0][2]);
+        const float v1 = j == 0 ? xo[1][0] : (j == 1 ? xo[1][1] : xo[1][2]);
+        const int n = 4 * j + g;
+        if (n < D) {
+          sX[n] = v0;
+          sX[12 + n] = v1;
+        }
+      }
+      sg_wsync();
 
-    // ================= NTN backward =================
-    const float gmk = (kv & (m > 0.f)) ? (INTENDED ? gs * Uk : gs * usum) : 0.f;
-    if (g == 0) {
-      gbn += gmk;
-      gUa += INTENDED ? gs * rk : gs * rsum;
-    }
-    float ge[2][3];   // dL/dx (before the x > 0 mask)
-    {
-      float x1[D];
+      // ================= NTN head (layers.py:282-310) =================
+      float x2[D];
 #pragma unroll
-      for (int a = 0; a < D; ++a) x1[a] = sX[a];
+      for (int b = 0; b < D; ++b) x2[b] = sX[12 + b];
+      float u[3];
+      float mpart = 0.f;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         const int a = 4 * r + g;
         const int ac = a < D ? a : 0;
-        const float c = gmk * xo[0][r];
+        const float *wa = sWa + (ac * FK + kc) * 12;
+        float acc = 0.f;
 #pragma unroll
-        for (int b = 0; b < D; ++b) gWn[r][b] = fmaf(c, x2[b], gWn[r][b]);
-        gVa[r] = fmaf(gmk, xo[0][r], gVa[r]);
-        gVb[r] = fmaf(gmk, xo[1][r], gVb[r]);
-        const float t1 = gmk * (sV[kc * 24 + ac] + u[r]);
-        const float *wb = sWb + (ac * FK + kc) * 12;
-        float w = 0.f;
-#pragma unroll
-        for (int aa = 0; aa < D; ++aa) w = fmaf(x1[aa], wb[aa], w);
-        const float t2 = gmk * (sV[kc * 24 + D + ac] + w);
-        ge[0][r] = row_sum16(t1) * A.ik4;
-        ge[1][r] = row_sum16(t2) * A.ik4;
+        for (int b = 0; b < D; ++b) acc = fmaf(wa[b], x2[b], acc);
+        u[r] = acc;
+        // x1[a] u[a][k] + V[k][a] x1[a] + V[k][D+a] x2[a]   (x of invalid a is 0)
+        mpart = fmaf(xo[0][r], acc + sV[kc * 24 + ac], mpart);
+        mpart = fmaf(xo[1][r], sV[kc * 24 + D + ac], mpart);
       }
-    }
+      float m = mpart + __shfl_xor(mpart, 16, 64);
+      m = m + __shfl_xor(m, 32, 64) + bnk;
+      const float rk = (kv & (m > 0.f)) ? m : 0.f;
+      const float rsum = row_sum16(rk);
+      const float sv = INTENDED ? row_sum16(Uk * rk) : usum * rsum;
+      if (!BWD) {
+        if (l == 0) A.s_out[p] = sv;
+        return;
+      }
+      if (A.s_out && l == 0) A.s_out[p] = sv;
+      const float yhat = expf(-A.yeta * sv * sv);
+      float gy;
+      if (!ALIGNED) {
+        gy = yhat - ybar;
+        lossa += 0.5f * gy * gy;
+      } else {
+        const float dl = yhat - sRec[2 * D * D + 2 * D + 2];
+        gy = dl * A.inv_batch;
+        lossa += 0.5f * dl * dl * A.inv_batch;
+      }
+      const float gs = gy * (-2.f * A.yeta * sv * yhat);
 
-    // ================= GCN backward =================
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bool big = s ? big1 : big0;
-      f4 gh2;
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        const float gp = xo[s][r] > 0.f ? ge[s][r] : 0.f;   // dropout4 · relu' · present
-        gwda = fmaf(d2[s][r], gp, gwda);
-        gbda += j == 0 ? gp : 0.f;
-        const float v = ((kb >> (3 * s + r)) & 1u) ? gp * wdv * A.ik2 : 0.f;
-        gb1a += v;
-        gh2[r] = v;
+      // ================= NTN backward =================
+      const float gmk = (kv & (m > 0.f)) ? (INTENDED ? gs * Uk : gs * usum) : 0.f;
+      if (g == 0) {
+        gbn += gmk;
+        gUa += INTENDED ? gs * rk : gs * rsum;
       }
-      gh2[3] = 0.f;
-      // gZ1 = Âᵀ gH2 in both orientations (Â symmetric, checked at pack time):
-      //   gz1  rows = nodes (B of gW1 = D1ᵀ gZ1),  gz1t rows = j (A of gD1 = gZ1 W1ᵀ)
-      f4 gz1 = {0.f, 0.f, 0.f, 0.f}, gz1t = {0.f, 0.f, 0.f, 0.f};
-      gz1 = mfma4(af[s][0], gh2[0], gz1);
-      gz1t = mfma4(gh2[0], af[s][0], gz1t);
-      gz1 = mfma4(af[s][1], gh2[1], gz1);
-      gz1t = mfma4(gh2[1], af[s][1], gz1t);
-      if (big) {
-        gz1 = mfma4(af[s][2], gh2[2], gz1);
-        gz1t = mfma4(gh2[2], af[s][2], gz1t);
-      }
-      // this lane's D1 entries: A operand of gW1 += D1ᵀ gZ1 and, as D1 > 0, the
-      // keep·relu' mask of gP1
-      const float *T1 = sT + s * 16 * TS1 + 4 * g * TS1 + j;
-      float dq[2][3];
+      const float gmk4 = gmk * A.ik4;
+      float ge[2][3];   // dL/dx · ik4 (before the x > 0 mask)
+      {
+        float x1[D];
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+        for (int a = 0; a < D; ++a) x1[a] = sX[a];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) dq[t][q] = T1[q * TS1 + 16 * t];
+        for (int r = 0; r < 3; ++r) {
+          const int a = 4 * r + g;
+          const int ac = a < D ? a : 0;
+          const float c = gmk * xo[0][r];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        gw1[t] = mfma4(dq[t][0], gz1[0], gw1[t]);
-        gw1[t] = mfma4(dq[t][1], gz1[1], gw1[t]);
-        if (big) gw1[t] = mfma4(dq[t][2], gz1[2], gw1[t]);
-      }
-      // one-hot Xᵀ rows for gW0: k-step q ↔ node 4q + g, row i = j ↔ type 16τ + j
-      float xo0[3], xo1[3];
+          for (int b = 0; b < D; ++b) gWn[r][b] = fmaf(c, x2[b], gWn[r][b]);
+          gVa[r] = fmaf(gmk, xo[0][r], gVa[r]);
+          gVb[r] = fmaf(gmk, xo[1][r], gVb[r]);
+          const float t1 = gmk4 * (sV[kc * 24 + ac] + u[r]);
+          const float *wb = sWb + (ac * FK + kc) * 12;
+          float w = 0.f;
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const int tq = (int)((tys[s] >> (6 * q)) & 63u);
-        xo0[q] = tq == j ? A.ik0 : 0.f;
-        xo1[q] = tq == 16 + j ? A.ik0 : 0.f;
-      }
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        f4 gd = {0.f, 0.f, 0.f, 0.f};  // gD1 = gZ1 W1ᵀ  (A = gZ1 from gz1t, B = W1[16t+j][4g+q])
-#pragma unroll
-        for (int q = 0; q < 4; ++q) gd = mfma4(gz1t[q], w1t[t][q], gd);
-        f4 gp1;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) gp1[r] = dq[t][r] > 0.f ? gd[r] * A.ik1 : 0.f;
-        gp1[3] = 0.f;
-        if (t) gb0a1 += gp1[0] + gp1[1] + gp1[2];
-        else gb0a0 += gp1[0] + gp1[1] + gp1[2];
-        f4 gz0 = {0.f, 0.f, 0.f, 0.f};  // gZ0 = Âᵀ gP1
-        gz0 = mfma4(af[s][0], gp1[0], gz0);
-        gz0 = mfma4(af[s][1], gp1[1], gz0);
-        if (big) gz0 = mfma4(af[s][2], gp1[2], gz0);
-        // gW0 += Xᵀ gZ0
-        gw0[0][t] = mfma4(xo0[0], gz0[0], gw0[0][t]);
-        gw0[1][t] = mfma4(xo1[0], gz0[0], gw0[1][t]);
-        gw0[0][t] = mfma4(xo0[1], gz0[1], gw0[0][t]);
-        gw0[1][t] = mfma4(xo1[1], gz0[1], gw0[1][t]);
-        if (big) {
-          gw0[0][t] = mfma4(xo0[2], gz0[2], gw0[0][t]);
-          gw0[1][t] = mfma4(xo1[2], gz0[2], gw0[1][t]);
+          for (int aa = 0; aa < D; ++aa) w = fmaf(x1[aa], wb[aa], w);
+          const float t2 = gmk4 * (sV[kc * 24 + D + ac] + w);
+          ge[0][r] = row_sum16(t1);
+          ge[1][r] = row_sum16(t2);
         }
       }
+
+      // ================= GCN backward =================
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int KS = s ? K1 : K0;
+        f4 gh2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < KS; ++r) {
+          const float gp = xo[s][r] > 0.f ? ge[s][r] : 0.f;   // dropout4 · relu' · present
+          gwda = fmaf(d2[s][r], gp, gwda);
+          gbda += gp;   // equal on the 16 lanes of a row: lane j == 0 is flushed
+          const float v = ((kb >> (3 * s + r)) & 1u) ? gp * wdv * A.ik2 : 0.f;
+          gb1a += v;
+          gh2[r] = v;
+        }
+        // gZ1 = Âᵀ gH2 in both orientations (Â symmetric, checked at pack time):
+        //   gz1  rows = nodes (B of gW1 = D1ᵀ gZ1),  gz1t rows = j (A of gD1 = gZ1 W1ᵀ)
+        f4 gz1 = {0.f, 0.f, 0.f, 0.f}, gz1t = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < KS; ++q) {
+          gz1 = mfma4(af[s][q], gh2[q], gz1);
+          gz1t = mfma4(gh2[q], af[s][q], gz1t);
+        }
+        // this lane's D1 entries: A operand of gW1 += D1ᵀ gZ1 and, as D1 > 0, the
+        // keep·relu' mask of gP1
+        const float *T1 = sT + s * 16 * TS1 + 4 * g * TS1 + j;
+        float dq[2][3];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int q = 0; q < KS; ++q) dq[t][q] = T1[q * TS1 + 16 * t];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int q = 0; q < KS; ++q) gw1[t] = mfma4(dq[t][q], gz1[q], gw1[t]);
+        // one-hot Xᵀ rows for gW0: k-step q ↔ node 4q + g, row i = j ↔ type 16τ + j
+        float xo0[3], xo1[3];
+#pragma unroll
+        for (int q = 0; q < KS; ++q) {
+          const int tq = (int)((tys[s] >> (6 * q)) & 63u);
+          xo0[q] = tq == j ? 1.f : 0.f;
+          xo1[q] = tq == 16 + j ? 1.f : 0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const f4 wt = *(const f4 *)(w1tp + 16 * t * W1S);
+          f4 gd = {0.f, 0.f, 0.f, 0.f};  // gD1 · ik1 = gZ1 (W1 ik1)ᵀ
+#pragma unroll
+          for (int q = 0; q < 4; ++q) gd = mfma4(gz1t[q], wt[q], gd);
+          f4 gp1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int r = 0; r < KS; ++r) gp1[r] = dq[t][r] > 0.f ? gd[r] : 0.f;
+          if (t) gb0a1 += (gp1[0] + gp1[1]) + gp1[2];
+          else gb0a0 += (gp1[0] + gp1[1]) + gp1[2];
+          f4 gz0 = {0.f, 0.f, 0.f, 0.f};  // gZ0 = Âᵀ gP1
+#pragma unroll
+          for (int q = 0; q < KS; ++q) gz0 = mfma4(af[s][q], gp1[q], gz0);
+#pragma unroll
+          for (int q = 0; q < KS; ++q) {  // gW0 / ik0 += Xᵀ gZ0
+            gw0[0][t] = mfma4(xo0[q], gz0[q], gw0[0][t]);
+            gw0[1][t] = mfma4(xo1[q], gz0[q], gw0[1][t]);
+          }
+        }
+      }
+    };
+    const bool big0 = N0 > 8, big1 = N1 > 8;
+    if (big0) {
+      if (big1) body(std::integral_constant<int, 3>{}, std::integral_constant<int, 3>{});
+      else body(std::integral_constant<int, 3>{}, std::integral_constant<int, 2>{});
+    } else {
+      if (big1) body(std::integral_constant<int, 2>{}, std::integral_constant<int, 3>{});
+      else body(std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{});
     }
   }
+
   if (!BWD) return;
   // ---- flush: one wave at a time into the workgroup slab row (deterministic) ----
   __syncthreads();
@@ -500,7 +532,7 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
       atomicAdd(&G[A.ob0 + 16 + j], gb0a1);
       atomicAdd(&G[A.ob1 + j], gb1a);
       atomicAdd(&G[A.oWd + j], gwda);
-      atomicAdd(&G[A.obd], gbda);
+      if (j == 0) atomicAdd(&G[A.obd], gbda);
       if (kv) {
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
@@ -524,7 +556,7 @@ __global__ void __launch_bounds__(512) sg_fast_kernel(FastArgs A) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int ty_ = 16 * tau + 4 * g + r;
-            if (ty_ < d_in) G[A.oW0 + ty_ * FH1 + 16 * t + j] += gw0[tau][t][r];
+            if (ty_ < d_in) G[A.oW0 + ty_ * FH1 + 16 * t + j] += gw0[tau][t][r] * A.ik0;
           }
       if (l == 0) G[A.n_params] += lossa;
     }
@@ -552,13 +584,13 @@ FastCfg fast_cfg_t(int d_in, int64_t n_pairs) {
   int best = 1, best_res = 0;
   const char *ev = getenv("SG_FAST_WAVES");
   const int force = ev ? atoi(ev) : 0;
-  for (int nw = 1; nw <= 8; ++nw) {
+  for (int nw = 1; nw <= MAXW; ++nw) {
     if (force > 0 && nw != force) continue;
     const size_t lds = (size_t)(c.shared_floats + nw * c.wave_floats) * 4u;
     if (lds > 163840u) break;
     int per_cu = (int)(163840u / lds);
     int res = per_cu * nw;
-    if (res > 8) res = 8;  // register-limited occupancy (2 waves/SIMD at 250 VGPRs)
+    if (res > MAXW) res = MAXW;  // register-limited occupancy: the block's waves per CU
     if (res > best_res || (res == best_res && nw > best)) {
       best = nw;
       best_res = res;
@@ -617,7 +649,7 @@ template <int D, bool BWD, bool ALIGNED, bool INTENDED>
 static void launch_one(const FastCfg &c, const FastArgs &A, hipStream_t st) {
   const void *fn = (const void *)sg_fast_kernel<D, BWD, ALIGNED, INTENDED>;
   if (c.lds > 65536u)
-    hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds);
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds);
   hipLaunchKernelGGL((sg_fast_kernel<D, BWD, ALIGNED, INTENDED>), dim3(c.blocks),
                      dim3(64 * c.waves), c.lds, st, A);
 }

@@ -511,7 +511,7 @@ int sg_generic_run(const SgGenPlan &P, bool bwd, const void *recs, int64_t n_pai
   A.s_out = s_out;
   A.slab = slab;
   if (L.lds_bytes > 65536u) {
-    hipFuncSetAttribute(bwd ? (const void *)sg_generic_kernel<true>
+    (void)hipFuncSetAttribute(bwd ? (const void *)sg_generic_kernel<true>
                             : (const void *)sg_generic_kernel<false>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
   }

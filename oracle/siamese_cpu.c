@@ -32,8 +32,8 @@ static inline uint32_t sg_mix(uint32_t x) {
 }
 static inline int keep_draw(uint32_t pk, uint32_t layer, uint32_t side, uint32_t e, uint32_t thr) {
   if (thr >= 65536u) return 1;
-  uint32_t h = sg_mix(((layer << 26) | (side << 25) | (e >> 1)) ^ pk);
-  uint32_t d = (e & 1u) ? (h >> 16) : (h & 0xFFFFu);
+  uint32_t h = sg_mix(((layer << 26) | e) ^ pk);   /* one hash: side 0 low, side 1 high */
+  uint32_t d = side ? (h >> 16) : (h & 0xFFFFu);
   return d < thr;
 }
 

@@ -57,16 +57,19 @@ def dropout_mask(seed: int, pair: int, side: int, layer: int, count: int,
 
     Replaces TF's `floor(keep_prob + random_uniform(shape))` (layers.py:334-336,
     tf.nn.dropout) with draw(seed, pair, side, layer, e) < round(keep*65536), where
-    e is the row-major element index of the logical (unpadded) tensor.
+    e is the row-major element index of the logical (unpadded) tensor of one side.
+    One hash sg_mix(pk ^ (layer << 26 | e)) serves the element e of both sides:
+    its low 16 bits are side 0's draw, its high 16 bits side 1's.
     """
     if keep >= 1.0:
         return np.ones(count, dtype=bool)
+    assert count <= (1 << 26)
     thr = keep_threshold(keep)
     pk = sg_mix(np.uint64((pair & _M32) ^ seed_key(seed)))
     e = np.arange(count, dtype=np.uint64)
-    ctr = (np.uint64(layer) << np.uint64(26)) | (np.uint64(side) << np.uint64(25)) | (e >> np.uint64(1))
+    ctr = (np.uint64(layer) << np.uint64(26)) | e
     h = sg_mix(ctr ^ pk)
-    draw = (h >> (np.uint64(16) * (e & np.uint64(1)))) & np.uint64(0xFFFF)
+    draw = (h >> np.uint64(16 * int(side))) & np.uint64(0xFFFF)
     return draw < np.uint64(thr)
 
 
