@@ -369,23 +369,28 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       sg_wsync();
 
       // ================= NTN head (layers.py:282-310) =================
+      // x_s is zero past 4 K_s elements: terms with a zero factor are dropped
+      // (each is an exact fmaf(0, ·, acc) = acc)
+      constexpr int BL0 = 4 * K0 < D ? 4 * K0 : D, BL1 = 4 * K1 < D ? 4 * K1 : D;
       float x2[D];
 #pragma unroll
-      for (int b = 0; b < D; ++b) x2[b] = sX[12 + b];
+      for (int b = 0; b < BL1; ++b) x2[b] = sX[12 + b];
       float u[3];
       float mpart = 0.f;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         const int a = 4 * r + g;
         const int ac = a < D ? a : 0;
-        const float *wa = sWa + (ac * FK + kc) * 12;
-        float acc = 0.f;
+        if (r < K0) {
+          const float *wa = sWa + (ac * FK + kc) * 12;
+          float acc = 0.f;
 #pragma unroll
-        for (int b = 0; b < D; ++b) acc = fmaf(wa[b], x2[b], acc);
-        u[r] = acc;
-        // x1[a] u[a][k] + V[k][a] x1[a] + V[k][D+a] x2[a]   (x of invalid a is 0)
-        mpart = fmaf(xo[0][r], acc + sV[kc * 24 + ac], mpart);
-        mpart = fmaf(xo[1][r], sV[kc * 24 + D + ac], mpart);
+          for (int b = 0; b < BL1; ++b) acc = fmaf(wa[b], x2[b], acc);
+          u[r] = acc;
+          // x1[a] u[a][k] + V[k][a] x1[a] + V[k][D+a] x2[a]   (x of invalid a is 0)
+          mpart = fmaf(xo[0][r], acc + sV[kc * 24 + ac], mpart);
+        }
+        if (r < K1) mpart = fmaf(xo[1][r], sV[kc * 24 + D + ac], mpart);
       }
       float m = mpart + __shfl_xor(mpart, 16, 64);
       m = m + __shfl_xor(m, 32, 64) + bnk;
@@ -420,24 +425,28 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       {
         float x1[D];
 #pragma unroll
-        for (int a = 0; a < D; ++a) x1[a] = sX[a];
+        for (int a = 0; a < BL0; ++a) x1[a] = sX[a];
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
           const int a = 4 * r + g;
           const int ac = a < D ? a : 0;
-          const float c = gmk * xo[0][r];
+          if (r < K0) {
+            const float c = gmk * xo[0][r];
 #pragma unroll
-          for (int b = 0; b < D; ++b) gWn[r][b] = fmaf(c, x2[b], gWn[r][b]);
-          gVa[r] = fmaf(gmk, xo[0][r], gVa[r]);
-          gVb[r] = fmaf(gmk, xo[1][r], gVb[r]);
-          const float t1 = gmk4 * (sV[kc * 24 + ac] + u[r]);
-          const float *wb = sWb + (ac * FK + kc) * 12;
-          float w = 0.f;
+            for (int b = 0; b < BL1; ++b) gWn[r][b] = fmaf(c, x2[b], gWn[r][b]);
+            gVa[r] = fmaf(gmk, xo[0][r], gVa[r]);
+            const float t1 = gmk4 * (sV[kc * 24 + ac] + u[r]);
+            ge[0][r] = row_sum16(t1);
+          }
+          if (r < K1) {
+            gVb[r] = fmaf(gmk, xo[1][r], gVb[r]);
+            const float *wb = sWb + (ac * FK + kc) * 12;
+            float w = 0.f;
 #pragma unroll
-          for (int aa = 0; aa < D; ++aa) w = fmaf(x1[aa], wb[aa], w);
-          const float t2 = gmk4 * (sV[kc * 24 + D + ac] + w);
-          ge[0][r] = row_sum16(t1);
-          ge[1][r] = row_sum16(t2);
+            for (int aa = 0; aa < BL0; ++aa) w = fmaf(x1[aa], wb[aa], w);
+            const float t2 = gmk4 * (sV[kc * 24 + D + ac] + w);
+            ge[1][r] = row_sum16(t2);
+          }
         }
       }
 
