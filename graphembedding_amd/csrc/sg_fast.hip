@@ -91,6 +91,47 @@ struct FastLds {
 };
 
 
+// Flush slots of one lane: gW1 (8) | gW0/ik0 (16) | NTN dW (3 D) | dV (3 + 3) |
+// dbn, dU, loss | db0 (2), db1, dWd, dbd (pre-summed over row groups)
+template <int D>
+struct FlushSlots {
+  static constexpr int NS = 8 + 16 + 3 * D + 6 + 3 + 5;
+};
+
+// parameter index of slot s on lane l = 16 g + j, or -1 if the slot is padding
+template <int D>
+__device__ __forceinline__ int fast_param(const FastArgs &A, int s, int l) {
+  const int g = l >> 4, j = l & 15;
+  if (s < 8) return A.oW1 + (16 * (s >> 2) + 4 * g + (s & 3)) * FH2 + j;
+  s -= 8;
+  if (s < 16) {
+    const int ty = 16 * (s >> 3) + 4 * g + (s & 3);
+    return ty < A.d_in ? A.oW0 + ty * FH1 + 16 * ((s >> 2) & 1) + j : -1;
+  }
+  s -= 16;
+  if (s < 3 * D) {
+    const int a = 4 * (s / D) + g, b = s % D;
+    return (a < D && j < FK) ? A.oW + (a * D + b) * FK + j : -1;
+  }
+  s -= 3 * D;
+  if (s < 6) {
+    const int a = 4 * (s % 3) + g;
+    return (a < D && j < FK) ? A.oV + j * 2 * D + (s >= 3 ? D : 0) + a : -1;
+  }
+  s -= 6;
+  switch (s) {
+    case 0: return (g == 0 && j < FK) ? A.obn + j : -1;
+    case 1: return (g == 0 && j < FK) ? A.oU + j : -1;
+    case 2: return l == 0 ? A.n_params : -1;
+    case 3: return g == 0 ? A.ob0 + j : -1;
+    case 4: return g == 0 ? A.ob0 + 16 + j : -1;
+    case 5: return g == 0 ? A.ob1 + j : -1;
+    case 6: return g == 0 ? A.oWd + j : -1;
+    case 7: return l == 0 ? A.obd : -1;
+    default: return -1;
+  }
+}
+
 template <int D, bool BWD, bool ALIGNED, bool INTENDED>
 __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -525,54 +566,66 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   }
 
   if (!BWD) return;
-  // ---- flush: one wave at a time into the workgroup slab row (deterministic) ----
-  __syncthreads();
-  float *G = smem;  // the weight tables are dead now
-  for (int i = tid; i <= A.n_params; i += blockDim.x) G[i] = 0.f;
-  __syncthreads();
-  for (int w = 0; w < nw; ++w) {
-    if (wv == w) {
+  // ---- flush: every wave dumps its accumulator slots to LDS, all threads sum ----
+  // Slot s of lane (g, j) maps to at most one parameter (fast_param below) and
+  // every parameter is hit exactly once, so the slab row is written directly.
+  // Waves are summed in fixed order (deterministic).  The block owns the CU's
+  // LDS (one block per CU), so all its waves' slots fit (fast_cfg).
+  constexpr int NS = FlushSlots<D>::NS;
+  {
+    // per-feature bias / Dense gradients: sum the four row groups in registers
+    gb0a0 += __shfl_xor(gb0a0, 16, 64);
+    gb0a1 += __shfl_xor(gb0a1, 16, 64);
+    gb1a += __shfl_xor(gb1a, 16, 64);
+    gwda += __shfl_xor(gwda, 16, 64);
+    gbda += __shfl_xor(gbda, 16, 64);
+    gb0a0 += __shfl_xor(gb0a0, 32, 64);
+    gb0a1 += __shfl_xor(gb0a1, 32, 64);
+    gb1a += __shfl_xor(gb1a, 32, 64);
+    gwda += __shfl_xor(gwda, 32, 64);
+    gbda += __shfl_xor(gbda, 32, 64);
+  }
+  float *F = smem;
+  __syncthreads();   // every wave has left the pair loop: the tables are dead
+  {
+    float *Fw = F + (size_t)wv * NS * 64 + l;
+    int s = 0;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Fw[64 * s++] = gw1[t][r];
+#pragma unroll
+    for (int tau = 0; tau < 2; ++tau)
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) G[A.oW1 + (16 * t + 4 * g + r) * FH2 + j] += gw1[t][r];
-      sg_wsync();
-      atomicAdd(&G[A.ob0 + j], gb0a0);
-      atomicAdd(&G[A.ob0 + 16 + j], gb0a1);
-      atomicAdd(&G[A.ob1 + j], gb1a);
-      atomicAdd(&G[A.oWd + j], gwda);
-      if (j == 0) atomicAdd(&G[A.obd], gbda);
-      if (kv) {
+        for (int r = 0; r < 4; ++r) Fw[64 * s++] = gw0[tau][t][r] * A.ik0;
 #pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          const int a = 4 * r + g;
-          if (a < D) {
+    for (int r = 0; r < 3; ++r)
 #pragma unroll
-            for (int b = 0; b < D; ++b) G[A.oW + (a * D + b) * FK + j] += gWn[r][b];
-            G[A.oV + j * 2 * D + a] += gVa[r];
-            G[A.oV + j * 2 * D + D + a] += gVb[r];
-          }
-        }
-        if (g == 0) {
-          G[A.obn + j] += gbn;
-          G[A.oU + j] += gUa;
-        }
-      }
+      for (int b = 0; b < D; ++b) Fw[64 * s++] = gWn[r][b];
 #pragma unroll
-      for (int tau = 0; tau < 2; ++tau)
+    for (int r = 0; r < 3; ++r) Fw[64 * s++] = gVa[r];
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int ty_ = 16 * tau + 4 * g + r;
-            if (ty_ < d_in) G[A.oW0 + ty_ * FH1 + 16 * t + j] += gw0[tau][t][r] * A.ik0;
-          }
-      if (l == 0) G[A.n_params] += lossa;
-    }
-    __syncthreads();
+    for (int r = 0; r < 3; ++r) Fw[64 * s++] = gVb[r];
+    Fw[64 * s++] = gbn;
+    Fw[64 * s++] = gUa;
+    Fw[64 * s++] = lossa;
+    Fw[64 * s++] = gb0a0;
+    Fw[64 * s++] = gb0a1;
+    Fw[64 * s++] = gb1a;
+    Fw[64 * s++] = gwda;
+    Fw[64 * s++] = gbda;
   }
+  __syncthreads();
   float *dst = A.slab + (size_t)blockIdx.x * (size_t)(A.n_params + 1);
-  for (int i = tid; i <= A.n_params; i += blockDim.x) dst[i] = G[i];
+  for (int idx = tid; idx < NS * 64; idx += blockDim.x) {
+    const int prm_i = fast_param<D>(A, idx >> 6, idx & 63);
+    if (prm_i < 0) continue;
+    float acc = 0.f;
+    for (int w = 0; w < nw; ++w) acc += F[(size_t)w * NS * 64 + idx];
+    dst[prm_i] = acc;
+  }
 }
 
 struct FastCfg {
@@ -584,11 +637,14 @@ struct FastCfg {
 };
 
 template <int D>
-FastCfg fast_cfg_t(int d_in, int64_t n_pairs) {
+FastCfg fast_cfg_t(int d_in, int64_t n_pairs, bool bwd) {
   FastCfg c;
   c.D = D;
   c.shared_floats = FastLds<D>::shared_floats(d_in);
   c.wave_floats = FastLds<D>::wave_floats(d_in);
+  // resident waves per CU allowed by registers: the backward kernel uses up to
+  // 256 VGPRs (2 waves / SIMD), the forward-only one ~120 (4 waves / SIMD)
+  const int wcap = bwd ? MAXW : 2 * MAXW;
   // pick waves/block maximising resident waves per CU under 160 KiB of LDS
   int best = 1, best_res = 0;
   const char *ev = getenv("SG_FAST_WAVES");
@@ -597,9 +653,10 @@ FastCfg fast_cfg_t(int d_in, int64_t n_pairs) {
     if (force > 0 && nw != force) continue;
     const size_t lds = (size_t)(c.shared_floats + nw * c.wave_floats) * 4u;
     if (lds > 163840u) break;
+    if (bwd && (size_t)nw * FlushSlots<D>::NS * 256u > 163840u) break;   // flush slots fit
     int per_cu = (int)(163840u / lds);
     int res = per_cu * nw;
-    if (res > MAXW) res = MAXW;  // register-limited occupancy: the block's waves per CU
+    if (res > wcap) res = wcap;  // register-limited occupancy
     if (res > best_res || (res == best_res && nw > best)) {
       best = nw;
       best_res = res;
@@ -607,7 +664,17 @@ FastCfg fast_cfg_t(int d_in, int64_t n_pairs) {
   }
   c.waves = best;
   c.lds = (size_t)(c.shared_floats + best * c.wave_floats) * 4u;
-  const int per_cu = (int)(163840u / c.lds);
+  // resident blocks per CU: LDS- and register-limited (MAXW waves per CU); a
+  // grid of exactly that many blocks per CU pays the prologue/flush once per block
+  int per_cu = (int)(163840u / c.lds);
+  if (per_cu > wcap / best) per_cu = wcap / best;
+  if (per_cu < 1) per_cu = 1;
+  // the flush dumps every wave's accumulator slots into the block's LDS
+  const size_t fl = bwd ? (size_t)best * FlushSlots<D>::NS * 64u * 4u : 0u;
+  if (fl > c.lds) {
+    c.lds = fl;
+    per_cu = (int)(163840u / c.lds);
+  }
   const int64_t want = (n_pairs + best - 1) / best;
   const int64_t cap = (int64_t)sg_num_cus() * per_cu;
   c.blocks = (int)(want < cap ? (want > 0 ? want : 1) : cap);
@@ -645,12 +712,12 @@ int sg_fast_supported(const sg_model_t *m, const SgGenPlan &P) {
   return fast_shape(m, P) ? 1 : 0;
 }
 
-static FastCfg fast_cfg(int D, int d_in, int64_t n_pairs) {
-  return D == 12 ? fast_cfg_t<12>(d_in, n_pairs) : fast_cfg_t<10>(d_in, n_pairs);
+static FastCfg fast_cfg(int D, int d_in, int64_t n_pairs, bool bwd) {
+  return D == 12 ? fast_cfg_t<12>(d_in, n_pairs, bwd) : fast_cfg_t<10>(d_in, n_pairs, bwd);
 }
 
 int64_t sg_fast_slab_floats(const SgGenPlan &P, int64_t n_pairs) {
-  FastCfg c = fast_cfg(P.n_max, P.d_in, n_pairs);
+  FastCfg c = fast_cfg(P.n_max, P.d_in, n_pairs, true);
   return (int64_t)c.blocks * (P.n_params + 1);
 }
 
@@ -683,7 +750,7 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
                 uint64_t seed, const float *y_stats, float *s_out, float *slab, int *blocks_out,
                 hipStream_t stream) {
   const int D = P.n_max;
-  FastCfg c = fast_cfg(D, P.d_in, n_pairs);
+  FastCfg c = fast_cfg(D, P.d_in, n_pairs, bwd);
   FastArgs A;
   A.recs = (const uint8_t *)recs;
   A.n_pairs = n_pairs;
@@ -720,8 +787,6 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
   A.oV = P.offV;
   A.oU = P.offU;
   A.obn = P.offB;
-  // the flush reuses the shared weight tables as the slab-row buffer
-  if ((size_t)c.shared_floats < (size_t)P.n_params + 1) return SG_ERR_UNSUPPORTED;
   const bool aligned = m->loss_mode == SG_LOSS_ALIGNED;
   const bool intended = m->ntn_mode == SG_NTN_INTENDED;
   if (D == 12) launch_fast<12>(c, bwd, aligned, intended, A, stream);

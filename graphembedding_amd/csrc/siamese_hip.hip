@@ -40,6 +40,7 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
 namespace {
 
 constexpr int kReduceStrands = 16;  // second-level partial rows
+constexpr int kOnePassRows = 1024;  // slabs up to this many rows reduce in one launch
 
 // slab [nblk][C] → part [S][C]; strand order fixed ⇒ bitwise reproducible.
 __global__ void __launch_bounds__(256) sg_reduce_stage1(const float *__restrict__ slab, int nblk,
@@ -55,6 +56,42 @@ __global__ void __launch_bounds__(256) sg_reduce_stage1(const float *__restrict_
   __syncthreads();
   if (w == 0 && col < C)
     part[(size_t)blockIdx.y * C + col] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+// slab [nblk][C] → grad[C-1], loss in one pass (nblk <= kOnePassRows): block x owns
+// columns 64x .. 64x+63; wave w of 16 sums rows w + 16 i into four independent
+// partials (i mod 4), combined in fixed order (deterministic)
+__global__ void __launch_bounds__(1024) sg_reduce_one(const float *__restrict__ slab, int nblk, int C,
+                                                      float *__restrict__ grad,
+                                                      float *__restrict__ loss,
+                                                      const float *__restrict__ y_stats,
+                                                      int add_label) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (col < C) {
+    const float *p = slab + col;
+    int b = w;
+    for (; b + 48 < nblk; b += 64) {
+      a0 += p[(size_t)b * C];
+      a1 += p[(size_t)(b + 16) * C];
+      a2 += p[(size_t)(b + 32) * C];
+      a3 += p[(size_t)(b + 48) * C];
+    }
+    for (; b < nblk; b += 16) a0 += p[(size_t)b * C];
+  }
+  red[w][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (w == 0 && col < C) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += red[k][lane];
+    if (col < C - 1)
+      grad[col] = v;
+    else if (loss)
+      loss[0] = v + ((add_label && y_stats) ? y_stats[1] : 0.f);
+  }
 }
 
 // part [S][C] → grad[C-1], loss = part[:, C-1] (+ label term)
@@ -192,6 +229,11 @@ __global__ void __launch_bounds__(1024) sg_adam_kernel(float *__restrict__ th, f
 
 int launch_reduce(const float *slab, int nblk, int C, float *part, float *grad, float *loss,
                   const float *y_stats, int add_label, hipStream_t st) {
+  if (nblk <= kOnePassRows) {   // the fused kernel's one-block-per-CU slabs
+    hipLaunchKernelGGL(sg_reduce_one, dim3((C + 63) / 64), dim3(1024), 0, st, slab, nblk, C, grad,
+                       loss, y_stats, add_label);
+    return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
+  }
   const int S = nblk < kReduceStrands ? (nblk > 0 ? nblk : 1) : kReduceStrands;
   hipLaunchKernelGGL(sg_reduce_stage1, dim3((C + 63) / 64, S), dim3(256), 0, st, slab, nblk, C, part);
   hipLaunchKernelGGL(sg_reduce_stage2, dim3((C + 255) / 256), dim3(256), 0, st, part, S, C, grad,
