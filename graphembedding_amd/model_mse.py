@@ -102,8 +102,12 @@ class SiameseGCNTNMSE(object):
         self.adam_v = torch.zeros_like(self.params)
         self.beta1, self.beta2, self.eps = 0.9, 0.999, 1e-8
         self.beta_powers = torch.tensor([self.beta1, self.beta2], dtype=torch.float32, device=device)
-        self.grad = torch.zeros_like(self.params)
-        self.loss_buf = torch.zeros(2, dtype=torch.float32, device=device)
+        # grad and loss_mse share one flat buffer: the data-parallel all-reduce
+        # (shard.make_allreduce_hook) is then a single in-place collective
+        n = self.params.numel()
+        self.grad_loss = torch.zeros(n + 2, dtype=torch.float32, device=device)
+        self.grad = self.grad_loss[:n]
+        self.loss_buf = self.grad_loss[n:]
         self.reg_buf = torch.zeros(1, dtype=torch.float32, device=device)
         self._ws = None
         self._ws_pairs = -1

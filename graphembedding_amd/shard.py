@@ -19,22 +19,21 @@ def shard_range(n_items: int, rank: int, world: int) -> Tuple[int, int]:
 
 
 def make_allreduce_hook(group=None):
-    """Model.grad_hook: sum grad and loss_mse over ranks (one fused buffer)."""
-    import torch
+    """Model.grad_hook: sum grad and loss_mse over ranks.  They are adjacent in
+    model.grad_loss, so this is one in-place all-reduce (RCCL over xGMI)."""
     import torch.distributed as dist
 
-    state = {}
-
     def hook(model):
+        buf = getattr(model, 'grad_loss', None)
         n = model.grad.numel()
-        buf = state.get('buf')
-        if buf is None or buf.numel() != n + 1 or buf.device != model.grad.device:
-            buf = torch.empty(n + 1, dtype=torch.float32, device=model.grad.device)
-            state['buf'] = buf
-        buf[:n].copy_(model.grad)
-        buf[n:].copy_(model.loss_buf[:1])
-        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
-        model.grad.copy_(buf[:n])
-        model.loss_buf[:1].copy_(buf[n:])
+        if (buf is not None and model.grad.data_ptr() == buf.data_ptr()
+                and model.loss_buf.data_ptr() == buf[n:].data_ptr()):
+            dist.all_reduce(buf[:n + 1], op=dist.ReduceOp.SUM, group=group)
+            return
+        import torch
+        tmp = torch.cat([model.grad, model.loss_buf[:1]])
+        dist.all_reduce(tmp, op=dist.ReduceOp.SUM, group=group)
+        model.grad.copy_(tmp[:n])
+        model.loss_buf[:1].copy_(tmp[n:])
 
     return hook

@@ -25,9 +25,19 @@ def test_shard_range_partitions():
 
 
 class _FakeModel:
-    def __init__(self, grad, loss):
-        self.grad = torch.tensor(grad, dtype=torch.float32)
-        self.loss_buf = torch.tensor([loss, 0.0], dtype=torch.float32)
+    """grad / loss_buf either separate tensors or views of one grad_loss buffer
+    (SiameseGCNTNMSE's layout, reduced by one in-place all-reduce)."""
+    def __init__(self, grad, loss, shared=False):
+        if shared:
+            n = len(grad)
+            self.grad_loss = torch.zeros(n + 2, dtype=torch.float32)
+            self.grad = self.grad_loss[:n]
+            self.loss_buf = self.grad_loss[n:]
+            self.grad.copy_(torch.tensor(grad, dtype=torch.float32))
+            self.loss_buf[0] = loss
+        else:
+            self.grad = torch.tensor(grad, dtype=torch.float32)
+            self.loss_buf = torch.tensor([loss, 0.0], dtype=torch.float32)
 
 
 def _free_port():
@@ -38,7 +48,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, shared=False):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
@@ -53,7 +63,7 @@ def _worker(rank, world, port, q):
         _, g, loss = cpu_ref.fwd_bwd_records(words[s0:e0], prob.n_max, prob.d_in, prob.params,
                                              77, 0.9, prob.flags.yeta, ybar, pair_offset=s0,
                                              threads=1)
-        m = _FakeModel(g, loss)
+        m = _FakeModel(g, loss, shared)
         make_allreduce_hook()(m)
         _, g_full, loss_full = cpu_ref.fwd_bwd_records(words, prob.n_max, prob.d_in,
                                                        prob.params, 77, 0.9, prob.flags.yeta,
@@ -65,11 +75,12 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_two_rank_gloo_step_equals_single_process():
+@pytest.mark.parametrize('shared', [False, True])
+def test_two_rank_gloo_step_equals_single_process(shared):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, shared)) for r in range(2)]
     for p in procs:
         p.start()
     out = [q.get(timeout=300) for _ in procs]
