@@ -31,6 +31,8 @@ def parse():
     p.add_argument('--warmup', type=int, default=3)
     p.add_argument('--dataset', default='syn_aids700nef')
     p.add_argument('--dropout', type=float, default=0.1)
+    p.add_argument('--records', choices=('f32', 'bf16'), default='f32',
+                   help='storage of Â in the pair records (bf16 = config C3); math is fp32')
     p.add_argument('--cpu-sample', type=int, default=0,
                    help='pairs for the CPU baseline (0 = auto, -1 = skip)')
     p.add_argument('--json-out', default='')
@@ -65,11 +67,11 @@ def main():
     from graphembedding_amd.model_mse import SiameseGCNTNMSE
     from graphembedding_amd.shard import make_allreduce_hook
 
-    flags = Flags(dropout=args.dropout)
+    flags = Flags(dropout=args.dropout, record_dtype=args.records)
     gs = load_graph_set(args.dataset, n_max=10)
     labels = gs.label_matrix(flags.yeta)
     model = SiameseGCNTNMSE(gs.d_in, flags, device=device, n_max=gs.n_max)
-    shard = AllPairsShard(gs, labels, rank, world, device=device)
+    shard = AllPairsShard(gs, labels, rank, world, device=device, dtype=args.records)
     batch = shard.batch(model)
     hook = make_allreduce_hook() if world > 1 else None
     model.workspace(batch.n_pairs)
@@ -123,7 +125,7 @@ def main():
         achieved_gbs = kern_pairs_s * bytes_pair / 1e9
         traffic = None
         tj = os.path.join(ROOT, 'profiles', 'traffic.json')
-        if model.kernel_path == 1 and os.path.isfile(tj):
+        if model.kernel_path == 1 and args.records == 'f32' and os.path.isfile(tj):
             with open(tj) as f:
                 t = json.load(f)
             # HBM bytes per launch from the committed PMC passes of this command
@@ -153,6 +155,7 @@ def main():
                                    'default 5-layer Siamese GCN-NTN, dropout {}'.format(args.dropout),
                        'global_batch': total_pairs, 'n_max': gs.n_max, 'd_in': gs.d_in,
                        'kernel_path': 'fused' if model.kernel_path == 1 else 'generic',
+                       'records': '{} Â, {} B/pair'.format(args.records, bytes_pair),
                        'parallelism': 'dp{}'.format(world)},
             'roofline': {'bound': 'mfma', 'achieved': achieved_tf, 'peak': FP32_PEAK_TFLOPS,
                          'unit': 'TFLOP/s', 'frac': achieved_tf / FP32_PEAK_TFLOPS,

@@ -38,7 +38,7 @@ class SgModel(ctypes.Structure):
                 ('n_max', ctypes.c_int32), ('final_act', ctypes.c_int32),
                 ('loss_mode', ctypes.c_int32), ('ntn_mode', ctypes.c_int32),
                 ('keep_prob', ctypes.c_float), ('yeta', ctypes.c_float),
-                ('layers', SgLayer * SG_MAX_LAYERS)]
+                ('layers', SgLayer * SG_MAX_LAYERS), ('adj_dtype', ctypes.c_int32)]
 
 
 class SiameseHipError(RuntimeError):
@@ -64,14 +64,20 @@ def lib():
     L.sg_version.restype = c_i32
     L.sg_record_bytes.argtypes = [c_i32]
     L.sg_record_bytes.restype = c_i64
+    L.sg_record_bytes_ex.argtypes = [c_i32, c_i32]
+    L.sg_record_bytes_ex.restype = c_i64
     L.sg_model_validate.argtypes = [pm, ctypes.POINTER(c_i64), ctypes.POINTER(c_i32)]
     L.sg_model_validate.restype = c_i32
     L.sg_workspace_bytes.argtypes = [pm, c_i64]
     L.sg_workspace_bytes.restype = c_i64
     L.sg_pack_pairs.argtypes = [vp, vp, vp, c_i32, c_i32, vp, vp, c_i64, vp, vp, vp]
     L.sg_pack_pairs.restype = c_i32
+    L.sg_pack_pairs_ex.argtypes = [vp, vp, vp, c_i32, c_i32, c_i32, vp, vp, c_i64, vp, vp, vp]
+    L.sg_pack_pairs_ex.restype = c_i32
     L.sg_label_stats.argtypes = [vp, c_i64, c_i32, vp, vp, vp]
     L.sg_label_stats.restype = c_i32
+    L.sg_label_stats_ex.argtypes = [vp, c_i64, c_i32, c_i32, vp, vp, vp]
+    L.sg_label_stats_ex.restype = c_i32
     L.sg_forward.argtypes = [pm, vp, c_i64, c_i64, vp, c_u64, vp, vp, vp]
     L.sg_forward.restype = c_i32
     L.sg_fwd_bwd.argtypes = [pm, vp, c_i64, c_i64, c_i64, vp, c_u64, vp, c_i32, vp, vp, vp, vp, vp]
@@ -82,8 +88,20 @@ def lib():
     return L
 
 
-EXPORTED_SYMBOLS = ('sg_version', 'sg_record_bytes', 'sg_model_validate', 'sg_workspace_bytes',
-                    'sg_pack_pairs', 'sg_label_stats', 'sg_forward', 'sg_fwd_bwd', 'sg_adam_tf')
+EXPORTED_SYMBOLS = ('sg_version', 'sg_record_bytes', 'sg_record_bytes_ex', 'sg_model_validate',
+                    'sg_workspace_bytes', 'sg_pack_pairs', 'sg_pack_pairs_ex', 'sg_label_stats',
+                    'sg_label_stats_ex', 'sg_forward', 'sg_fwd_bwd', 'sg_adam_tf')
+
+# sg_dtype: storage type of Â in the pair records
+DTYPES = {'f32': 0, 'bf16': 1}
+
+
+def dtype_code(dtype) -> int:
+    if isinstance(dtype, int):
+        return dtype
+    if dtype not in DTYPES:
+        raise RuntimeError('Unknown record dtype {}'.format(dtype))
+    return DTYPES[dtype]
 
 
 def check(rc: int, what: str) -> None:
@@ -107,7 +125,7 @@ def final_act_code(final_act: str, sim_kernel: str) -> int:
 
 def make_model(layers: List[dict], d_in: int, n_max: int, keep_prob: float, final_act: str,
                sim_kernel: str, yeta: float, loss_mode: str = 'broadcast',
-               ntn_mode: str = 'reference') -> SgModel:
+               ntn_mode: str = 'reference', adj_dtype='f32') -> SgModel:
     """Layer dicts (graphembedding_amd.layers_factory format) → sg_model_t."""
     if len(layers) > SG_MAX_LAYERS:
         raise RuntimeError('at most {} layers supported'.format(SG_MAX_LAYERS))
@@ -118,6 +136,7 @@ def make_model(layers: List[dict], d_in: int, n_max: int, keep_prob: float, fina
     m.final_act = final_act_code(final_act, sim_kernel)
     m.loss_mode = {'broadcast': LOSS_BROADCAST, 'aligned': LOSS_ALIGNED}[loss_mode]
     m.ntn_mode = {'reference': NTN_REFERENCE, 'intended': NTN_INTENDED}[ntn_mode]
+    m.adj_dtype = dtype_code(adj_dtype)
     m.keep_prob = float(keep_prob)
     m.yeta = float(yeta if yeta is not None else 0.0)
     for i, L in enumerate(layers):
@@ -156,8 +175,8 @@ def validate(m: SgModel):
     return int(n.value), int(p.value)
 
 
-def record_bytes(n_max: int) -> int:
-    return int(lib().sg_record_bytes(int(n_max)))
+def record_bytes(n_max: int, dtype='f32') -> int:
+    return int(lib().sg_record_bytes_ex(int(n_max), dtype_code(dtype)))
 
 
 def _ptr(t) -> Optional[int]:
@@ -179,17 +198,19 @@ def workspace_bytes(m: SgModel, n_pairs: int) -> int:
 
 
 def pack_pairs(store_adj, store_types, store_n, n_max, pair_idx, labels, records, status=None,
-               stream=None):
+               stream=None, dtype='f32'):
     n_graphs = int(store_n.shape[0])
     n_pairs = int(pair_idx.shape[0])
-    check(lib().sg_pack_pairs(_ptr(store_adj), _ptr(store_types), _ptr(store_n), n_graphs,
-                              int(n_max), _ptr(pair_idx), _ptr(labels), n_pairs, _ptr(records),
-                              _ptr(status), _stream(stream)), 'sg_pack_pairs')
+    check(lib().sg_pack_pairs_ex(_ptr(store_adj), _ptr(store_types), _ptr(store_n), n_graphs,
+                                 int(n_max), dtype_code(dtype), _ptr(pair_idx), _ptr(labels),
+                                 n_pairs, _ptr(records), _ptr(status), _stream(stream)),
+          'sg_pack_pairs_ex')
 
 
-def label_stats(records, n_pairs, n_max, stats_out, workspace, stream=None):
-    check(lib().sg_label_stats(_ptr(records), int(n_pairs), int(n_max), _ptr(stats_out),
-                               _ptr(workspace), _stream(stream)), 'sg_label_stats')
+def label_stats(records, n_pairs, n_max, stats_out, workspace, stream=None, dtype='f32'):
+    check(lib().sg_label_stats_ex(_ptr(records), int(n_pairs), int(n_max), dtype_code(dtype),
+                                  _ptr(stats_out), _ptr(workspace), _stream(stream)),
+          'sg_label_stats_ex')
 
 
 def forward(m: SgModel, records, n_pairs, pair_offset, params, seed, s_out, workspace=None,

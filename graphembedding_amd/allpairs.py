@@ -64,7 +64,7 @@ class AllPairsShard(object):
     """This rank's slice of the all-pairs stream, packed once into HBM."""
 
     def __init__(self, gs: GraphSet, labels: np.ndarray, rank: int = 0, world: int = 1,
-                 device='cuda', n_pairs: Optional[int] = None):
+                 device='cuda', n_pairs: Optional[int] = None, dtype: str = 'f32'):
         import torch
         G = len(gs.graphs)
         self.total = int(n_pairs if n_pairs is not None else G * G)
@@ -73,7 +73,8 @@ class AllPairsShard(object):
         pairs = np.stack([p // G, p % G], axis=1).astype(np.int32)
         flat_labels = labels.reshape(-1)[:self.total]
         lab = flat_labels[self.start:self.end]
-        self.records, status = pack_device(gs.store, pairs, lab, device=device)
+        self.dtype = dtype
+        self.records, status = pack_device(gs.store, pairs, lab, device=device, dtype=dtype)
         torch.cuda.synchronize()
         if int(status.item()) != 0:
             raise RuntimeError('sg_pack_pairs reported invalid graph ids')
@@ -83,7 +84,7 @@ class AllPairsShard(object):
         self.y_stats = torch.tensor([ybar, 0.5 * ((y - ybar) ** 2).sum()], dtype=torch.float32,
                                     device=device)
         self.n = self.end - self.start
-        self.record_bytes = 4 * record_words(gs.n_max)
+        self.record_bytes = 4 * record_words(gs.n_max, dtype)
 
     def batch(self, model, rank: int = 0):
         return model.batch_from_records(self.records, self.n, self.labels,

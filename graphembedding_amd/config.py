@@ -56,6 +56,7 @@ DEFAULTS: Dict[str, Any] = dict(
     label_stream='compat',     # 'compat' = labels from a later sampler draw (A3) | 'aligned'
     test_matrix='full',        # 'full' = sim_mat[i][j] | 'compat_diag' = sim_mat[i][i] (A5)
     n_max=None,                # record node capacity (default: Padding max_in_dims or data max)
+    record_dtype='f32',        # storage of Â in pair records: 'f32' | 'bf16' (config C3); fp32 math
     seed=123,                  # dropout RNG base seed (the reference's TF RNG was unseeded)
     param_seed=0,              # glorot init seed
 )

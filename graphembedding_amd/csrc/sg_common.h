@@ -111,25 +111,40 @@ __device__ __forceinline__ float sg_wave_sum(float v) {
   return v;
 }
 
-// Pair record field offsets in 4-byte words (see siamese_hip.h).
+// Pair record field offsets in 4-byte words (see siamese_hip.h).  The HBM
+// record stores Â as f32 or bf16 (adj_dtype); kernels stage every record into
+// LDS in the f32 layout (sg_rec_layout(n_max)).
 struct SgRecLayout {
   int n_max;
-  int words;      // record size in 4-byte words
-  int adj;        // [2][n_max][n_max] f32
+  int dtype;      // sg_dtype of Â
+  int words;      // record size in 4-byte words (multiple of 4: 16-B records)
+  int adj;        // [2][n_max][n_max] f32, or bf16 packed two per word
+  int adj_words;  // 2 n_max² (f32) or n_max² (bf16)
   int types;      // [2][n_max] i32
   int nnodes;     // [2] i32
   int label;      // f32
   int tag;        // i32
 };
 
-static inline SgRecLayout sg_rec_layout(int n_max) {
+static inline SgRecLayout sg_rec_layout(int n_max, int dtype = SG_DTYPE_F32) {
   SgRecLayout r;
   r.n_max = n_max;
+  r.dtype = dtype;
   r.adj = 0;
-  r.types = 2 * n_max * n_max;
+  r.adj_words = dtype == SG_DTYPE_BF16 ? n_max * n_max : 2 * n_max * n_max;
+  r.types = r.adj_words;
   r.nnodes = r.types + 2 * n_max;
   r.label = r.nnodes + 2;
   r.tag = r.label + 1;
-  r.words = r.tag + 1;
+  r.words = (r.tag + 1 + 3) & ~3;
   return r;
+}
+
+static inline bool sg_dtype_ok(int dtype) { return dtype == SG_DTYPE_F32 || dtype == SG_DTYPE_BF16; }
+
+// bf16 (RNE) of an f32, the record encoding of SG_DTYPE_BF16 (NaN-free inputs)
+__host__ __device__ __forceinline__ uint32_t sg_f32_to_bf16(float f) {
+  uint32_t u;
+  __builtin_memcpy(&u, &f, 4);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
 }

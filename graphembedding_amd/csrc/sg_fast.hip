@@ -64,6 +64,8 @@ struct FastArgs {
   const uint8_t *recs;
   int64_t n_pairs;
   int64_t pair_offset;
+  int rw4h;      // 16-B words per HBM record (f32 or bf16 Â)
+  int rec_bf16;  // Â stored as bf16: widened to the f32 LDS layout while staging
   const float *params;
   const float *y_stats;
   float *s_out;
@@ -233,21 +235,42 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 
   const int64_t stride = (int64_t)gridDim.x * nw;
   int64_t p = (int64_t)blockIdx.x * nw + wv;
+  // HBM record: rw4h 16-B words (RW4 for f32 Â, fewer for bf16 Â)
+  const int rw4h = A.rw4h;
+  constexpr int ADJ4 = D * D / 4;   // 16-B words of a bf16 adjacency block (D even)
   uint4 pre[NREC];
 #pragma unroll
   for (int c = 0; c < NREC; ++c) {
     const int w4 = l + 64 * c;
-    pre[c] = (p < A.n_pairs && w4 < RW4)
-                 ? ((const uint4 *)(A.recs + (size_t)p * (L::RW * 4)))[w4]
+    pre[c] = (p < A.n_pairs && w4 < rw4h)
+                 ? ((const uint4 *)(A.recs + (size_t)p * (size_t)rw4h * 16u))[w4]
                  : uint4{0u, 0u, 0u, 0u};
   }
 
   for (; p < A.n_pairs; p += stride) {
     sg_wsync();
+    if (A.rec_bf16) {
 #pragma unroll
-    for (int c = 0; c < NREC; ++c) {
-      const int w4 = l + 64 * c;
-      if (w4 < RW4) ((uint4 *)sRec)[w4] = pre[c];
+      for (int c = 0; c < NREC; ++c) {
+        const int w4 = l + 64 * c;
+        const uint4 v = pre[c];
+        if (w4 < ADJ4) {   // 8 bf16 entries of Â → 8 f32
+          f4 lo = {__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xFFFF0000u),
+                   __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xFFFF0000u)};
+          f4 hi = {__uint_as_float(v.z << 16), __uint_as_float(v.z & 0xFFFF0000u),
+                   __uint_as_float(v.w << 16), __uint_as_float(v.w & 0xFFFF0000u)};
+          ((f4 *)sRec)[2 * w4] = lo;
+          ((f4 *)sRec)[2 * w4 + 1] = hi;
+        } else if (w4 < rw4h) {
+          ((uint4 *)sRec)[w4 + ADJ4] = v;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < NREC; ++c) {
+        const int w4 = l + 64 * c;
+        if (w4 < RW4) ((uint4 *)sRec)[w4] = pre[c];
+      }
     }
     sg_wsync();
     {
@@ -255,8 +278,8 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #pragma unroll
       for (int c = 0; c < NREC; ++c) {
         const int w4 = l + 64 * c;
-        if (pn < A.n_pairs && w4 < RW4)
-          pre[c] = ((const uint4 *)(A.recs + (size_t)pn * (L::RW * 4)))[w4];
+        if (pn < A.n_pairs && w4 < rw4h)
+          pre[c] = ((const uint4 *)(A.recs + (size_t)pn * (size_t)rw4h * 16u))[w4];
       }
     }
     const int *ty = (const int *)sRec;
@@ -754,6 +777,8 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
   FastArgs A;
   A.recs = (const uint8_t *)recs;
   A.n_pairs = n_pairs;
+  A.rw4h = P.hbm_words / 4;
+  A.rec_bf16 = P.adj_dtype == SG_DTYPE_BF16 ? 1 : 0;
   A.pair_offset = pair_offset;
   A.params = params;
   A.y_stats = y_stats;

@@ -328,9 +328,22 @@ __global__ void __launch_bounds__(256) sg_generic_kernel(SgGenPlan P, GenArgs A)
   const float ybar = (BWD && P.loss_mode == SG_LOSS_BROADCAST) ? A.y_stats[0] : 0.f;
   float loss_acc = 0.f;
   for (int64_t p = (int64_t)blockIdx.x * nw + wave; p < A.n_pairs; p += (int64_t)gridDim.x * nw) {
-    const uint32_t *rec = (const uint32_t *)(A.recs + (size_t)p * (size_t)P.rec_words * 4u);
+    const uint32_t *rec = (const uint32_t *)(A.recs + (size_t)p * (size_t)P.hbm_words * 4u);
     uint32_t *R = (uint32_t *)(S + P.l_rec);
-    for (int i = lane; i < P.rec_words; i += SG_WAVE) R[i] = rec[i];
+    if (P.adj_dtype == SG_DTYPE_BF16) {   // widen Â to the f32 LDS layout
+      const int aw = P.hbm_adj_words;
+      for (int i = lane; i < P.hbm_words; i += SG_WAVE) {
+        const uint32_t v = rec[i];
+        if (i < aw) {
+          R[2 * i] = v << 16;
+          R[2 * i + 1] = v & 0xFFFF0000u;
+        } else if (i - aw < P.rec_words - 2 * aw) {
+          R[i + aw] = v;
+        }
+      }
+    } else {
+      for (int i = lane; i < P.rec_words; i += SG_WAVE) R[i] = rec[i];
+    }
     sg_wsync();
     const float *adj = S + P.l_rec;
     const int *types = (const int *)(S + P.l_rec + P.rec_types);

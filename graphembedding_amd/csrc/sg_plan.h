@@ -37,7 +37,8 @@ struct SgGenPlan {
   int l_rec, l_x12, l_u, l_m, l_gm, l_tmp, l_tmp2, l_g0, l_g1;
   int wave_floats;             // per-wave LDS floats
   int n_params;
-  int n_max, rec_words, rec_types, rec_nnodes, rec_label;
+  int n_max, rec_words, rec_types, rec_nnodes, rec_label;   // LDS (f32) record layout
+  int adj_dtype, hbm_words, hbm_adj_words;                  // HBM record (sg_dtype of Â)
   int d_in;
   int final_act, loss_mode, ntn_mode;
   float yeta;
@@ -54,9 +55,14 @@ static int sg_build_plan(const sg_model_t *m, SgGenPlan *P) {
   if (m->final_act < SG_FINAL_GAUSSIAN || m->final_act > SG_FINAL_TANH) return SG_ERR_ARG;
   if (m->loss_mode != SG_LOSS_BROADCAST && m->loss_mode != SG_LOSS_ALIGNED) return SG_ERR_ARG;
   if (m->ntn_mode != SG_NTN_REFERENCE && m->ntn_mode != SG_NTN_INTENDED) return SG_ERR_ARG;
+  if (!sg_dtype_ok(m->adj_dtype)) return SG_ERR_ARG;
   const int nmax = m->n_max;
   const SgRecLayout rl = sg_rec_layout(nmax);
+  const SgRecLayout rh = sg_rec_layout(nmax, m->adj_dtype);
   P->n_max = nmax;
+  P->adj_dtype = m->adj_dtype;
+  P->hbm_words = rh.words;
+  P->hbm_adj_words = rh.adj_words;
   P->rec_words = rl.words;
   P->rec_types = rl.types;
   P->rec_nnodes = rl.nnodes;

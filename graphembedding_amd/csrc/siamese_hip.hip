@@ -155,11 +155,13 @@ __global__ void __launch_bounds__(256) sg_label_final(const double *__restrict__
   }
 }
 
-// ---- pair packing: one wave per pair, record words copied lane-parallel ----
+// ---- pair packing: one wave per pair, record words written lane-parallel ----
+// Â is stored as f32 or as bf16 pairs (sg_dtype); the rest of the record is the
+// same words after the adjacency block, then zero padding to 16 B.
 __global__ void __launch_bounds__(256) sg_pack_kernel(const float *__restrict__ sadj,
                                                       const int32_t *__restrict__ stypes,
                                                       const int32_t *__restrict__ sn, int n_graphs,
-                                                      int nmax, const int32_t *__restrict__ pidx,
+                                                      int nmax, int bf16, const int32_t *__restrict__ pidx,
                                                       const float *__restrict__ labels, int64_t n,
                                                       uint32_t *__restrict__ recs, int rec_words,
                                                       int32_t *__restrict__ status) {
@@ -170,22 +172,31 @@ __global__ void __launch_bounds__(256) sg_pack_kernel(const float *__restrict__ 
   const bool bad = g0 < 0 || g0 >= n_graphs || g1 < 0 || g1 >= n_graphs;
   if (bad && lane == 0 && status) atomicExch(status, (int32_t)SG_ERR_ARG);
   const int nn = nmax * nmax;
+  const int aw = bf16 ? nn : 2 * nn;               // adjacency words
+  const int tail = 2 * nmax + 4;                    // types, n_nodes, label, tag
   uint32_t *dst = recs + (size_t)p * rec_words;
+  auto adj_at = [&](int e) -> float {               // e in [0, 2 nn): side e / nn
+    const int s = e / nn, o = e - s * nn;
+    return sadj[(size_t)(s ? g1 : g0) * nn + o];
+  };
   for (int w = lane; w < rec_words; w += SG_WAVE) {
     uint32_t v = 0u;
     if (!bad) {
-      if (w < 2 * nn) {
-        const int s = w / nn, o = w - s * nn;
-        v = __float_as_uint(sadj[(size_t)(s ? g1 : g0) * nn + o]);
-      } else if (w < 2 * nn + 2 * nmax) {
-        const int o = w - 2 * nn, s = o / nmax, i = o - s * nmax;
-        v = (uint32_t)stypes[(size_t)(s ? g1 : g0) * nmax + i];
-      } else if (w < 2 * nn + 2 * nmax + 2) {
-        v = (uint32_t)sn[(w == 2 * nn + 2 * nmax) ? g0 : g1];
-      } else if (w == 2 * nn + 2 * nmax + 2) {
-        v = __float_as_uint(labels ? labels[p] : 0.f);
-      } else {
-        v = (uint32_t)(p & 0x7FFFFFFF);
+      if (w < aw) {
+        v = bf16 ? (sg_f32_to_bf16(adj_at(2 * w)) | (sg_f32_to_bf16(adj_at(2 * w + 1)) << 16))
+                 : __float_as_uint(adj_at(w));
+      } else if (w < aw + tail) {
+        const int o = w - aw;
+        if (o < 2 * nmax) {
+          const int s = o / nmax, i = o - s * nmax;
+          v = (uint32_t)stypes[(size_t)(s ? g1 : g0) * nmax + i];
+        } else if (o < 2 * nmax + 2) {
+          v = (uint32_t)sn[(o == 2 * nmax) ? g0 : g1];
+        } else if (o == 2 * nmax + 2) {
+          v = __float_as_uint(labels ? labels[p] : 0.f);
+        } else {
+          v = (uint32_t)(p & 0x7FFFFFFF);
+        }
       }
     }
     dst[w] = v;
@@ -267,11 +278,13 @@ PathChoice choose_path(const sg_model_t *m, bool bwd) {
 // ===========================================================================
 extern "C" {
 
-int32_t sg_version(void) { return 10000; }
+int32_t sg_version(void) { return 10100; }   /* 1.1.0: bf16 Â records */
 
-int64_t sg_record_bytes(int32_t n_max) {
-  if (n_max <= 0) return 0;
-  return (int64_t)sg_rec_layout(n_max).words * 4;
+int64_t sg_record_bytes(int32_t n_max) { return sg_record_bytes_ex(n_max, SG_DTYPE_F32); }
+
+int64_t sg_record_bytes_ex(int32_t n_max, int32_t adj_dtype) {
+  if (n_max <= 0 || !sg_dtype_ok(adj_dtype)) return 0;
+  return (int64_t)sg_rec_layout(n_max, adj_dtype).words * 4;
 }
 
 int32_t sg_model_validate(const sg_model_t *model, int64_t *n_params_out, int32_t *path_out) {
@@ -303,24 +316,41 @@ int32_t sg_pack_pairs(const float *store_adj, const int32_t *store_types, const 
                       int32_t n_graphs, int32_t n_max, const int32_t *pair_idx,
                       const float *labels, int64_t n_pairs, void *records,
                       int32_t *status_out, sg_stream_t stream) {
+  return sg_pack_pairs_ex(store_adj, store_types, store_n, n_graphs, n_max, SG_DTYPE_F32, pair_idx,
+                          labels, n_pairs, records, status_out, stream);
+}
+
+int32_t sg_pack_pairs_ex(const float *store_adj, const int32_t *store_types,
+                         const int32_t *store_n, int32_t n_graphs, int32_t n_max,
+                         int32_t adj_dtype, const int32_t *pair_idx, const float *labels,
+                         int64_t n_pairs, void *records, int32_t *status_out,
+                         sg_stream_t stream) {
   if (n_pairs < 0 || n_max <= 0 || n_max > 64 || n_graphs <= 0) return SG_ERR_ARG;
+  if (!sg_dtype_ok(adj_dtype)) return SG_ERR_ARG;
   if (n_pairs == 0) return SG_OK;
   if (!store_adj || !store_types || !store_n || !pair_idx || !records) return SG_ERR_ARG;
-  const SgRecLayout rl = sg_rec_layout(n_max);
+  const SgRecLayout rl = sg_rec_layout(n_max, adj_dtype);
   const int wpb = 4;
   const int64_t blocks = (n_pairs + wpb - 1) / wpb;
   if (blocks > 0x7FFFFFFF) return SG_ERR_ARG;
   hipLaunchKernelGGL(sg_pack_kernel, dim3((unsigned)blocks), dim3(64 * wpb), 0, (hipStream_t)stream,
-                     store_adj, store_types, store_n, n_graphs, n_max, pair_idx, labels, n_pairs,
+                     store_adj, store_types, store_n, n_graphs, n_max,
+                     adj_dtype == SG_DTYPE_BF16 ? 1 : 0, pair_idx, labels, n_pairs,
                      (uint32_t *)records, rl.words, status_out);
   return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
 }
 
 int32_t sg_label_stats(const void *records, int64_t n_pairs, int32_t n_max, float *stats_out,
                        void *workspace, sg_stream_t stream) {
+  return sg_label_stats_ex(records, n_pairs, n_max, SG_DTYPE_F32, stats_out, workspace, stream);
+}
+
+int32_t sg_label_stats_ex(const void *records, int64_t n_pairs, int32_t n_max, int32_t adj_dtype,
+                          float *stats_out, void *workspace, sg_stream_t stream) {
   if (!records || !stats_out || !workspace || n_pairs <= 0 || n_max <= 0 || n_max > 64)
     return SG_ERR_ARG;
-  const SgRecLayout rl = sg_rec_layout(n_max);
+  if (!sg_dtype_ok(adj_dtype)) return SG_ERR_ARG;
+  const SgRecLayout rl = sg_rec_layout(n_max, adj_dtype);
   hipStream_t st = (hipStream_t)stream;
   double *part = (double *)workspace;
   double *mean = part + 256;

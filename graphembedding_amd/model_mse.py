@@ -89,8 +89,10 @@ class SiameseGCNTNMSE(object):
             pass
         self.sim_kernel = create_sim_kernel(f.sim_kernel, f.yeta)
         self.final_act_np = create_activation(f.final_act, self.sim_kernel)
+        self.record_dtype = getattr(f, 'record_dtype', 'f32') or 'f32'
         self.sg = _lib.make_model(self.layers, self.input_dim, self.n_max, 1.0 - f.dropout,
-                                  f.final_act, f.sim_kernel, f.yeta, f.loss_mode, f.ntn_mode)
+                                  f.final_act, f.sim_kernel, f.yeta, f.loss_mode, f.ntn_mode,
+                                  self.record_dtype)
         self.n_params, self.kernel_path = _lib.validate(self.sg)
         import torch
         self.torch = torch
@@ -171,7 +173,7 @@ class SiameseGCNTNMSE(object):
                 idx[k, c] = index[id(g)]
         store = GraphStore(uniq, self.n_max, self.input_dim)
         lab = np.zeros(len(g1s), np.float32) if labels is None else np.asarray(labels, np.float32)
-        words = store.pack_host(idx, lab)
+        words = store.pack_host(idx, lab, dtype=self.record_dtype)
         recs = torch.from_numpy(words.view(np.int32).reshape(-1)).to(self.device)
         gids = np.array([[a.nxgraph.graph.get('gid', -1), b.nxgraph.graph.get('gid', -1)]
                          for a, b in zip(g1s, g2s)])

@@ -15,12 +15,31 @@ from typing import Optional, Sequence
 import numpy as np
 
 
-def record_words(n_max: int) -> int:
-    return 2 * n_max * n_max + 2 * n_max + 4
+def adj_words(n_max: int, dtype: str = 'f32') -> int:
+    """Words of the Â block: f32 entries, or bf16 entries packed two per word."""
+    return n_max * n_max if dtype == 'bf16' else 2 * n_max * n_max
 
 
-def record_bytes(n_max: int) -> int:
-    return 4 * record_words(n_max)
+def record_words(n_max: int, dtype: str = 'f32') -> int:
+    """Record words, padded to 16 B (include/siamese_hip.h)."""
+    if dtype not in ('f32', 'bf16'):
+        raise RuntimeError('Unknown record dtype {}'.format(dtype))
+    return (adj_words(n_max, dtype) + 2 * n_max + 4 + 3) & ~3
+
+
+def record_bytes(n_max: int, dtype: str = 'f32') -> int:
+    return 4 * record_words(n_max, dtype)
+
+
+def f32_to_bf16_bits(x: np.ndarray) -> np.ndarray:
+    """RNE float32 → bf16 bit patterns (uint16), the SG_DTYPE_BF16 encoding."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+
+
+def bf16_round(x: np.ndarray) -> np.ndarray:
+    """Values of f32 → bf16 → f32 (what a bf16 record's kernels compute with)."""
+    return (f32_to_bf16_bits(x).astype(np.uint32) << 16).view(np.float32)
 
 
 class GraphStore(object):
@@ -58,29 +77,36 @@ class GraphStore(object):
                          torch.from_numpy(self.n).to(device))
         return self._dev
 
-    def pack_host(self, pair_idx: np.ndarray, labels: Optional[np.ndarray] = None) -> np.ndarray:
-        """Host twin of sg_pack_pairs: uint32 words [n_pairs][record_words]."""
+    def pack_host(self, pair_idx: np.ndarray, labels: Optional[np.ndarray] = None,
+                  dtype: str = 'f32') -> np.ndarray:
+        """Host twin of sg_pack_pairs_ex: uint32 words [n_pairs][record_words]."""
         pair_idx = np.asarray(pair_idx, dtype=np.int64).reshape(-1, 2)
         P = pair_idx.shape[0]
         nm = self.n_max
-        W = record_words(nm)
+        W = record_words(nm, dtype)
         out = np.zeros((P, W), dtype=np.uint32)
         a, b = pair_idx[:, 0], pair_idx[:, 1]
         nn = nm * nm
-        out[:, 0:nn] = self.adj[a].reshape(P, nn).view(np.uint32)
-        out[:, nn:2 * nn] = self.adj[b].reshape(P, nn).view(np.uint32)
-        out[:, 2 * nn:2 * nn + nm] = self.types[a].view(np.uint32)
-        out[:, 2 * nn + nm:2 * nn + 2 * nm] = self.types[b].view(np.uint32)
-        out[:, 2 * nn + 2 * nm] = self.n[a].view(np.uint32)
-        out[:, 2 * nn + 2 * nm + 1] = self.n[b].view(np.uint32)
+        adj = np.concatenate([self.adj[a].reshape(P, nn), self.adj[b].reshape(P, nn)], axis=1)
+        if dtype == 'bf16':
+            bits = f32_to_bf16_bits(adj).astype(np.uint32)             # [P, 2 nn]
+            out[:, 0:nn] = bits[:, 0::2] | (bits[:, 1::2] << 16)
+        else:
+            out[:, 0:2 * nn] = adj.view(np.uint32)
+        o = adj_words(nm, dtype)
+        out[:, o:o + nm] = self.types[a].view(np.uint32)
+        out[:, o + nm:o + 2 * nm] = self.types[b].view(np.uint32)
+        out[:, o + 2 * nm] = self.n[a].view(np.uint32)
+        out[:, o + 2 * nm + 1] = self.n[b].view(np.uint32)
         lab = np.zeros(P, np.float32) if labels is None else np.asarray(labels, np.float32)
-        out[:, 2 * nn + 2 * nm + 2] = lab.view(np.uint32)
-        out[:, 2 * nn + 2 * nm + 3] = (np.arange(P) & 0x7FFFFFFF).astype(np.uint32)
+        out[:, o + 2 * nm + 2] = lab.view(np.uint32)
+        out[:, o + 2 * nm + 3] = (np.arange(P) & 0x7FFFFFFF).astype(np.uint32)
         return out
 
 
-def pack_device(store: GraphStore, pair_idx, labels=None, device='cuda', stream=None):
-    """Device packing via sg_pack_pairs. pair_idx: int32 [n,2] (numpy or torch)."""
+def pack_device(store: GraphStore, pair_idx, labels=None, device='cuda', stream=None,
+                dtype: str = 'f32'):
+    """Device packing via sg_pack_pairs_ex. pair_idx: int32 [n,2] (numpy or torch)."""
     import torch
     from . import _lib
     adj, types, n = store.to_device(device)
@@ -89,20 +115,28 @@ def pack_device(store: GraphStore, pair_idx, labels=None, device='cuda', stream=
     lab = None
     if labels is not None:
         lab = torch.as_tensor(labels, dtype=torch.float32, device=device).reshape(-1).contiguous()
-    recs = torch.empty(P * record_words(store.n_max), dtype=torch.int32, device=device)
+    recs = torch.empty(P * record_words(store.n_max, dtype), dtype=torch.int32, device=device)
     status = torch.zeros(1, dtype=torch.int32, device=device)
     if P:
-        _lib.pack_pairs(adj, types, n, store.n_max, pi, lab, recs, status, stream=stream)
+        _lib.pack_pairs(adj, types, n, store.n_max, pi, lab, recs, status, stream=stream,
+                        dtype=dtype)
     return recs, status
 
 
-def unpack_host(words: np.ndarray, n_max: int):
-    """Split host record words into fields (for tests / debugging)."""
-    words = np.asarray(words, dtype=np.uint32).reshape(-1, record_words(n_max))
+def unpack_host(words: np.ndarray, n_max: int, dtype: str = 'f32'):
+    """Split host record words into fields (for tests / debugging); a bf16 Â is
+    returned widened to f32."""
+    words = np.asarray(words, dtype=np.uint32).reshape(-1, record_words(n_max, dtype))
     nn = n_max * n_max
-    adj = words[:, :2 * nn].view(np.float32).reshape(-1, 2, n_max, n_max)
-    types = words[:, 2 * nn:2 * nn + 2 * n_max].view(np.int32).reshape(-1, 2, n_max)
-    n = words[:, 2 * nn + 2 * n_max:2 * nn + 2 * n_max + 2].view(np.int32)
-    label = words[:, 2 * nn + 2 * n_max + 2].view(np.float32)
-    tag = words[:, 2 * nn + 2 * n_max + 3].view(np.int32)
+    if dtype == 'bf16':
+        a = words[:, :nn]
+        bits = np.stack([a << 16, a & 0xFFFF0000], axis=2).reshape(-1, 2 * nn)
+        adj = bits.astype(np.uint32).view(np.float32).reshape(-1, 2, n_max, n_max)
+    else:
+        adj = words[:, :2 * nn].view(np.float32).reshape(-1, 2, n_max, n_max)
+    o = adj_words(n_max, dtype)
+    types = words[:, o:o + 2 * n_max].view(np.int32).reshape(-1, 2, n_max)
+    n = words[:, o + 2 * n_max:o + 2 * n_max + 2].view(np.int32)
+    label = words[:, o + 2 * n_max + 2].view(np.float32)
+    tag = words[:, o + 2 * n_max + 3].view(np.int32)
     return dict(adj=adj, types=types, n=n, label=label, tag=tag)

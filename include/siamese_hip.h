@@ -81,6 +81,12 @@ enum sg_ntn_mode {
 
 #define SG_MAX_LAYERS 8
 
+/* Storage type of Â in the packed pair records (compute is fp32 either way). */
+typedef enum sg_dtype {
+  SG_DTYPE_F32 = 0,   /* 4 B per entry: the reference's float32 placeholders (A11) */
+  SG_DTYPE_BF16 = 1   /* 2 B per entry, RNE from f32: config C3, 496 B/pair at n_max 10 */
+} sg_dtype;
+
 typedef struct sg_layer {
   int32_t kind;          /* sg_layer_kind */
   int32_t input_dim;     /* GCN/Dense/Attention/NTN input width (GCN layer 0: d_in) */
@@ -102,6 +108,7 @@ typedef struct sg_model {
   float keep_prob;    /* 1 - FLAGS.dropout */
   float yeta;         /* FLAGS.yeta */
   sg_layer_t layers[SG_MAX_LAYERS];
+  int32_t adj_dtype;  /* sg_dtype of Â in the records passed to sg_forward / sg_fwd_bwd */
 } sg_model_t;
 
 /*
@@ -114,6 +121,15 @@ typedef struct sg_model {
  * sg_record_bytes(10) == 896.
  */
 int64_t sg_record_bytes(int32_t n_max);
+
+/*
+ * Record with Â stored as adj_dtype.  SG_DTYPE_BF16 layout:
+ *   uint16_t adj[2][n_max][n_max] (bf16, RNE of the f32 Â; 2·n_max² entries in
+ *            n_max² words), then types, n_nodes, label, tag as above, the record
+ *            padded to a multiple of 16 B.  sg_record_bytes_ex(10, BF16) == 496.
+ * The kernels widen Â to f32 while staging a record into LDS.
+ */
+int64_t sg_record_bytes_ex(int32_t n_max, int32_t adj_dtype);
 
 /* Library version (major*10000 + minor*100 + patch). */
 int32_t sg_version(void);
@@ -142,9 +158,20 @@ int32_t sg_pack_pairs(const float *store_adj, const int32_t *store_types, const 
                       const float *labels, int64_t n_pairs, void *records,
                       int32_t *status_out, sg_stream_t stream);
 
+/* sg_pack_pairs writing records with Â stored as adj_dtype (sg_dtype). */
+int32_t sg_pack_pairs_ex(const float *store_adj, const int32_t *store_types,
+                         const int32_t *store_n, int32_t n_graphs, int32_t n_max,
+                         int32_t adj_dtype, const int32_t *pair_idx, const float *labels,
+                         int64_t n_pairs, void *records, int32_t *status_out,
+                         sg_stream_t stream);
+
 /* stats_out[0] = mean label ȳ, stats_out[1] = ½Σ(y-ȳ)² over the n_pairs records. */
 int32_t sg_label_stats(const void *records, int64_t n_pairs, int32_t n_max, float *stats_out,
                        void *workspace, sg_stream_t stream);
+
+/* sg_label_stats over records with Â stored as adj_dtype. */
+int32_t sg_label_stats_ex(const void *records, int64_t n_pairs, int32_t n_max, int32_t adj_dtype,
+                          float *stats_out, void *workspace, sg_stream_t stream);
 
 /*
  * Forward only: s_out[i] = pre-activation score of record i (the test path:

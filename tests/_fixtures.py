@@ -50,8 +50,12 @@ class Problem:
                             weight_decay=f.weight_decay, dist_norm=f.dist_norm)
 
     def oracle_graphs(self):
-        gs = [O.Graph(adj=m.adj.astype(np.float32).astype(np.float64), types=m.types)
-              for m in self.mgs]
+        from graphembedding_amd.packer import bf16_round
+        rd = getattr(self.flags, 'record_dtype', 'f32')
+        # bf16 records store Â rounded to bf16 (RNE); the kernels compute with that Â
+        cast = (lambda a: bf16_round(a.astype(np.float32))) if rd == 'bf16' else \
+            (lambda a: a.astype(np.float32))
+        gs = [O.Graph(adj=cast(m.adj).astype(np.float64), types=m.types) for m in self.mgs]
         return [gs[i] for i in self.pairs[:, 0]], [gs[j] for j in self.pairs[:, 1]]
 
     def store(self) -> GraphStore:
@@ -62,7 +66,7 @@ class Problem:
         import torch
         model = SiameseGCNTNMSE(self.d_in, self.flags, device=device, n_max=self.n_max,
                                 params=self.params)
-        words = self.store().pack_host(self.pairs, self.labels)
+        words = self.store().pack_host(self.pairs, self.labels, dtype=model.record_dtype)
         recs = torch.from_numpy(words.view(np.int32).reshape(-1)).to(device)
         batch = model.batch_from_records(recs, len(self.pairs), self.labels)
         return model, batch

@@ -24,6 +24,9 @@ STACKS = {
                                     'dropout=True,bias=False'),
     'intended_aligned': dict(ntn_mode='intended', loss_mode='aligned'),
     'sigmoid_final': dict(final_act='sigmoid'),
+    # config C3: Â stored as bf16 in the records (fused path and generic path)
+    'default_bf16_records': dict(record_dtype='bf16'),
+    'average_bf16_records': dict(AVERAGE_STACK, record_dtype='bf16'),
 }
 
 
@@ -79,29 +82,33 @@ def test_large_batch_properties(gpu):
     _check_grad(g_sum, g_full.cpu().numpy(), tol=1e-5)
 
 
-def test_pack_pairs_device_matches_host(gpu):
+@pytest.mark.parametrize('dtype', ['f32', 'bf16'])
+def test_pack_pairs_device_matches_host(gpu, dtype):
     import torch
     from graphembedding_amd.packer import pack_device
     prob = small_problem(n_graphs=10, n_pairs=50, seed=2)
     store = prob.store()
-    words_h = store.pack_host(prob.pairs, prob.labels)
-    recs, status = pack_device(store, prob.pairs, prob.labels, device=gpu)
+    words_h = store.pack_host(prob.pairs, prob.labels, dtype=dtype)
+    recs, status = pack_device(store, prob.pairs, prob.labels, device=gpu, dtype=dtype)
     torch.cuda.synchronize()
     assert int(status.item()) == 0
     assert np.array_equal(recs.cpu().numpy().view(np.uint32).reshape(words_h.shape), words_h)
     bad = prob.pairs.copy()
     bad[3, 1] = 10_000
-    _, status = pack_device(store, bad, prob.labels, device=gpu)
+    _, status = pack_device(store, bad, prob.labels, device=gpu, dtype=dtype)
     assert int(status.item()) != 0
 
 
-def test_label_stats(gpu):
+@pytest.mark.parametrize('dtype', ['f32', 'bf16'])
+def test_label_stats(gpu, dtype):
     import torch
     from graphembedding_amd import _lib
-    prob = small_problem(n_graphs=10, n_pairs=3000, seed=4)
+    prob = small_problem(n_graphs=10, n_pairs=3000, seed=4,
+                         flags_overrides=dict(record_dtype=dtype))
     model, batch = prob.make_gpu_model(device=gpu)
     stats = torch.zeros(2, dtype=torch.float32, device=gpu)
-    _lib.label_stats(batch.records, batch.n_pairs, prob.n_max, stats, model.workspace(3000))
+    _lib.label_stats(batch.records, batch.n_pairs, prob.n_max, stats, model.workspace(3000),
+                     dtype=dtype)
     y = prob.labels.astype(np.float64)
     st = stats.cpu().numpy()
     assert abs(st[0] - y.mean()) < 1e-6

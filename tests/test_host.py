@@ -63,6 +63,27 @@ def test_packer_record_layout_and_padding():
         assert f['label'][k] == prob.labels[k] and f['tag'][k] == k
 
 
+def test_packer_bf16_records():
+    """Config C3: Â stored as bf16 (RNE), 496-B records, other fields unchanged."""
+    from graphembedding_amd.packer import bf16_round, record_bytes
+    prob = small_problem(n_graphs=6, n_pairs=9, seed=3)
+    store = prob.store()
+    assert record_bytes(10, 'bf16') == 496 and record_bytes(30, 'bf16') == 4 * (900 + 64)
+    assert record_bytes(11, 'bf16') % 16 == 0
+    w32 = store.pack_host(prob.pairs, prob.labels)
+    w16 = store.pack_host(prob.pairs, prob.labels, dtype='bf16')
+    assert w16.shape == (9, 124) and w16.nbytes == 9 * 496
+    f32, f16 = unpack_host(w32, 10), unpack_host(w16, 10, 'bf16')
+    assert np.array_equal(f16['adj'], bf16_round(f32['adj']))
+    for k in ('types', 'n', 'label', 'tag'):
+        assert np.array_equal(f16[k], f32[k]), k
+    # RNE: 1 + 2^-8 (a tie) rounds to even 1.0; 1 + 3·2^-9 rounds up
+    x = np.array([1.0 + 2 ** -8, 1.0 + 3 * 2 ** -9], np.float32)
+    assert list(bf16_round(x)) == [1.0, 1.0 + 2 ** -7]
+    with pytest.raises(RuntimeError, match='dtype'):
+        record_bytes(10, 'f16')
+
+
 def test_packer_rejects_oversize_graph():
     prob = small_problem(n_graphs=4, n_pairs=2, seed=1, n_lo=11, n_hi=12)
     with pytest.raises(RuntimeError, match='n_max'):

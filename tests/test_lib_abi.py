@@ -36,6 +36,8 @@ def test_record_layout(L):
     assert _lib.record_bytes(10) == 896          # 896 B per fp32 pair record
     assert _lib.record_bytes(30) == 4 * (2 * 900 + 60 + 4)
     assert _lib.record_bytes(0) == 0
+    assert _lib.record_bytes(10, 'bf16') == 496   # §8(d) bf16 figure (492) + tag word
+    assert L.sg_record_bytes_ex(10, 7) == 0       # unknown dtype
 
 
 def _model(prob, **kw):
