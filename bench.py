@@ -41,11 +41,15 @@ def parse():
 
 def cpu_baseline(gs, labels, flags, n_sample):
     """Time the oracle's C restatement (oracle/siamese_cpu.c, OpenMP) on a
-    bounded sample of the same all-pairs stream, on this host's cores."""
-    import numpy as np
+    bounded sample of the same all-pairs stream, on this host's cores (all of
+    them, and 1 thread as SURVEY §8(d) asks)."""
     sys.path.insert(0, os.path.join(ROOT, 'tests'))
     from oracle import cpu_ref
-    return cpu_ref.time_allpairs_sample(gs, labels, flags, n_sample)
+    out = cpu_ref.time_allpairs_sample(gs, labels, flags, n_sample)
+    one = cpu_ref.time_allpairs_sample(gs, labels, flags, 0, target_s=4.0, threads=1)
+    out['value_1thread'] = one['value']
+    out['sample_1thread'] = one['sample']
+    return out
 
 
 def main():

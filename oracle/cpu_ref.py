@@ -65,7 +65,8 @@ def default_threads() -> int:
         return max(1, os.cpu_count() or 1)
 
 
-def time_allpairs_sample(gs, labels, flags, n_sample: int = 0, target_s: float = 12.0):
+def time_allpairs_sample(gs, labels, flags, n_sample: int = 0, target_s: float = 12.0,
+                         threads: int = 0):
     """Time fwd+bwd of the C restatement on the all-pairs stream of `gs`.
     n_sample > 0: the first n_sample pairs once.  n_sample == 0 (auto): about
     target_s seconds of work — whole all-pairs passes repeated when one pass is
@@ -74,7 +75,7 @@ def time_allpairs_sample(gs, labels, flags, n_sample: int = 0, target_s: float =
     from graphembedding_amd.layers_factory import create_layers
     G = len(gs.graphs)
     total = G * G
-    threads = default_threads()
+    threads = threads if threads and threads > 0 else default_threads()
     layers = create_layers(flags, gs.d_in)
     params = glorot_flat(layers, gs.d_in, flags.param_seed)
     ybar = float(labels.astype(np.float64).mean())
