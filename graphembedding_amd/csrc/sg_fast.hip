@@ -214,6 +214,17 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       const int c = 4 * q + g;
       afo[s][q] = (ri < 3 && ni < D && c < D) ? L::REC + s * D * D + ni * D + c : L::X + 47;
     }
+  // Pairs with both sides <= 8 nodes share one 16-row tile in the feature products
+  // (D1·W1 and gZ1·W1ᵀ): tile rows with r = i % 4 < 2 are side 0's, rows with r >= 2
+  // side 1's row i - 2.  This lane's A row i = j comes from side jp, row jr.
+  const int jp = (j >> 1) & 1, jr = j - 2 * jp;
+  const float *sTp = sT + jp * 16 * TS1 + jr * TS1 + 8 * g;   // shared-tile D1 row j
+  int afp[2];   // side 1's Â row ni(j-2) on lanes jp = 1, zero elsewhere (B of the shared gZ1ᵀ)
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int nr = 4 * (jr & 3) + (jr >> 2), c = 4 * q + g;
+    afp[q] = (jp && nr < D && c < D) ? L::REC + D * D + nr * D + c : L::X + 47;
+  }
   int tyo[3];   // record word of the type of node 4r + g (side 0; side 1 at + D)
 #pragma unroll
   for (int r = 0; r < 3; ++r) tyo[r] = 2 * D * D + (4 * r + g < D ? 4 * r + g : 0);
@@ -375,22 +386,40 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         }
       }
       sg_wsync();   // rows 4g+3 of the tiles stay zero from the prologue
+      constexpr bool PACK = K0 == 2 && K1 == 2;   // both sides share the feature-product tile
       f4 h2[2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {   // Z1 = D1 W1 ; H2 = Â Z1 + b1
-        const int KS = s ? K1 : K0;
-        const float *T = sT + s * 16 * TS1 + j * TS1 + 8 * g;
-        const f4 lo = *(const f4 *)T, hi = *(const f4 *)(T + 4);
+      if constexpr (PACK) {   // Z1 of both sides in one 16-row tile; H2 = Â Z1 + b1 per side
+        const f4 lo = *(const f4 *)sTp, hi = *(const f4 *)(sTp + 4);
         const f4 wlo = *(const f4 *)w1bp, whi = *(const f4 *)(w1bp + 4);
         f4 z1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < 4; ++q) z1 = mfma4(lo[q], wlo[q], z1);
 #pragma unroll
         for (int q = 0; q < 4; ++q) z1 = mfma4(hi[q], whi[q], z1);
-        f4 acc = {b1v, b1v, b1v, b1v};
 #pragma unroll
-        for (int q = 0; q < KS; ++q) acc = mfma4(af[s][q], z1[q], acc);
-        h2[s] = acc;
+        for (int s = 0; s < 2; ++s) {
+          f4 acc = {b1v, b1v, b1v, b1v};
+          acc = mfma4(af[s][0], z1[2 * s], acc);
+          acc = mfma4(af[s][1], z1[2 * s + 1], acc);
+          h2[s] = acc;
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {   // Z1 = D1 W1 ; H2 = Â Z1 + b1
+          const int KS = s ? K1 : K0;
+          const float *T = sT + s * 16 * TS1 + j * TS1 + 8 * g;
+          const f4 lo = *(const f4 *)T, hi = *(const f4 *)(T + 4);
+          const f4 wlo = *(const f4 *)w1bp, whi = *(const f4 *)(w1bp + 4);
+          f4 z1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) z1 = mfma4(lo[q], wlo[q], z1);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) z1 = mfma4(hi[q], whi[q], z1);
+          f4 acc = {b1v, b1v, b1v, b1v};
+#pragma unroll
+          for (int q = 0; q < KS; ++q) acc = mfma4(af[s][q], z1[q], acc);
+          h2[s] = acc;
+        }
       }
       // D2 = dropout(H2) (one hash per element, both sides); zpre = D2·Wd + bd;
       // x = dropout(pad(relu(zpre))): row group g holds x_s[4r+g].  x > 0 exactly when
@@ -515,10 +544,12 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       }
 
       // ================= GCN backward =================
+      f4 gh2[2], gz1t[2];
+      float dq[2][2][3];   // [side][t][q]: this lane's D1 entries
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int KS = s ? K1 : K0;
-        f4 gh2 = {0.f, 0.f, 0.f, 0.f};
+        gh2[s] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int r = 0; r < KS; ++r) {
           const float gp = xo[s][r] > 0.f ? ge[s][r] : 0.f;   // dropout4 · relu' · present
@@ -526,28 +557,55 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           gbda += gp;   // equal on the 16 lanes of a row: lane j == 0 is flushed
           const float v = ((kb >> (3 * s + r)) & 1u) ? gp * wdv * A.ik2 : 0.f;
           gb1a += v;
-          gh2[r] = v;
+          gh2[s][r] = v;
         }
         // gZ1 = Âᵀ gH2 in both orientations (Â symmetric, checked at pack time):
         //   gz1  rows = nodes (B of gW1 = D1ᵀ gZ1),  gz1t rows = j (A of gD1 = gZ1 W1ᵀ)
-        f4 gz1 = {0.f, 0.f, 0.f, 0.f}, gz1t = {0.f, 0.f, 0.f, 0.f};
+        f4 gz1 = {0.f, 0.f, 0.f, 0.f};
+        gz1t[s] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < KS; ++q) {
-          gz1 = mfma4(af[s][q], gh2[q], gz1);
-          gz1t = mfma4(gh2[q], af[s][q], gz1t);
+          gz1 = mfma4(af[s][q], gh2[s][q], gz1);
+          if (!PACK) gz1t[s] = mfma4(gh2[s][q], af[s][q], gz1t[s]);
         }
         // this lane's D1 entries: A operand of gW1 += D1ᵀ gZ1 and, as D1 > 0, the
         // keep·relu' mask of gP1
         const float *T1 = sT + s * 16 * TS1 + 4 * g * TS1 + j;
-        float dq[2][3];
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int q = 0; q < KS; ++q) dq[t][q] = T1[q * TS1 + 16 * t];
+          for (int q = 0; q < KS; ++q) dq[s][t][q] = T1[q * TS1 + 16 * t];
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int q = 0; q < KS; ++q) gw1[t] = mfma4(dq[t][q], gz1[q], gw1[t]);
+          for (int q = 0; q < KS; ++q) gw1[t] = mfma4(dq[s][t][q], gz1[q], gw1[t]);
+      }
+      if constexpr (PACK) {
+        // gZ1ᵀ of both sides in the shared layout: side 0's Â rows are zero on the
+        // lanes of side 1's rows (nodes >= 8 are absent), afp holds side 1's rows there
+        f4 c = {0.f, 0.f, 0.f, 0.f};
+        c = mfma4(gh2[0][0], af[0][0], c);
+        c = mfma4(gh2[0][1], af[0][1], c);
+        c = mfma4(gh2[1][0], W[afp[0]], c);
+        c = mfma4(gh2[1][1], W[afp[1]], c);
+        gz1t[0] = c;
+      }
+      // gD1 · ik1 = gZ1 (W1 ik1)ᵀ per feature tile t (one chain per tile when packed)
+      f4 gd[2][2];   // [side, or 0 = shared][t]
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const f4 wt = *(const f4 *)(w1tp + 16 * t * W1S);
+#pragma unroll
+        for (int s = 0; s < (PACK ? 1 : 2); ++s) {
+          f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc = mfma4(gz1t[s][q], wt[q], acc);
+          gd[s][t] = acc;
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int KS = s ? K1 : K0;
         // one-hot Xᵀ rows for gW0: k-step q ↔ node 4q + g, row i = j ↔ type 16τ + j
         float xo0[3], xo1[3];
 #pragma unroll
@@ -558,13 +616,12 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const f4 wt = *(const f4 *)(w1tp + 16 * t * W1S);
-          f4 gd = {0.f, 0.f, 0.f, 0.f};  // gD1 · ik1 = gZ1 (W1 ik1)ᵀ
-#pragma unroll
-          for (int q = 0; q < 4; ++q) gd = mfma4(gz1t[q], wt[q], gd);
           f4 gp1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int r = 0; r < KS; ++r) gp1[r] = dq[t][r] > 0.f ? gd[r] : 0.f;
+          for (int r = 0; r < KS; ++r) {
+            const float gdv = PACK ? gd[0][t][2 * s + r] : gd[s][t][r];
+            gp1[r] = dq[s][t][r] > 0.f ? gdv : 0.f;
+          }
           if (t) gb0a1 += (gp1[0] + gp1[1]) + gp1[2];
           else gb0a0 += (gp1[0] + gp1[1]) + gp1[2];
           f4 gz0 = {0.f, 0.f, 0.f, 0.f};  // gZ0 = Âᵀ gP1
