@@ -51,6 +51,19 @@ __device__ __forceinline__ float dpp(float v) {
 }
 
 
+// x[l] + x[l ^ 16] and x[l] + x[l ^ 32]: gfx950 v_permlane16/32_swap leave x[l]
+// and its partner in the two registers (either order), one add completes the sum
+__device__ __forceinline__ float xsum16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false,
+                                                  false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xsum32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false,
+                                                  false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // Sum over the 16 lanes of a DPP row; result in every lane of the row.
 __device__ __forceinline__ float row_sum16(float v) {
   v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
@@ -485,8 +498,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         }
         if (r < K1) mpart = fmaf(xo[1][r], sV[kc * 24 + D + ac], mpart);
       }
-      float m = mpart + __shfl_xor(mpart, 16, 64);
-      m = m + __shfl_xor(m, 32, 64) + bnk;
+      const float m = xsum32(xsum16(mpart)) + bnk;
       const float rk = (kv & (m > 0.f)) ? m : 0.f;
       const float rsum = row_sum16(rk);
       const float sv = INTENDED ? row_sum16(Uk * rk) : usum * rsum;
@@ -495,7 +507,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         return;
       }
       if (A.s_out && l == 0) A.s_out[p] = sv;
-      const float yhat = expf(-A.yeta * sv * sv);
+      const float yhat = __expf(-A.yeta * sv * sv);   // v_exp_f32: ~1e-7 relative
       float gy;
       if (!ALIGNED) {
         gy = yhat - ybar;
@@ -654,16 +666,11 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   constexpr int NS = FlushSlots<D>::NS;
   {
     // per-feature bias / Dense gradients: sum the four row groups in registers
-    gb0a0 += __shfl_xor(gb0a0, 16, 64);
-    gb0a1 += __shfl_xor(gb0a1, 16, 64);
-    gb1a += __shfl_xor(gb1a, 16, 64);
-    gwda += __shfl_xor(gwda, 16, 64);
-    gbda += __shfl_xor(gbda, 16, 64);
-    gb0a0 += __shfl_xor(gb0a0, 32, 64);
-    gb0a1 += __shfl_xor(gb0a1, 32, 64);
-    gb1a += __shfl_xor(gb1a, 32, 64);
-    gwda += __shfl_xor(gwda, 32, 64);
-    gbda += __shfl_xor(gbda, 32, 64);
+    gb0a0 = xsum32(xsum16(gb0a0));
+    gb0a1 = xsum32(xsum16(gb0a1));
+    gb1a = xsum32(xsum16(gb1a));
+    gwda = xsum32(xsum16(gwda));
+    gbda = xsum32(xsum16(gbda));
   }
   float *F = smem;
   __syncthreads();   // every wave has left the pair loop: the tables are dead
