@@ -175,13 +175,10 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   float *sT = W + L::TILE;
   float *sX = W + L::X;
 
-  // Dropout scales (1/keep > 0) are folded into the linear maps that feed each
-  // dropped tensor, so the forward only selects: Z0 = (W0·ik0·ik1)[type] with
-  // b0·ik1 gives P1' = ik1·P1 and D1 = keep·relu(P1'); W1·ik2 with b1·ik2 gives
-  // H2' = ik2·H2 and D2 = keep·H2'; Wd·ik4, bd·ik4 give zpre' = ik4·zpre.  The
-  // backward uses the unscaled derivatives (gP1 from gZ1 (W1·ik1)ᵀ as before).
+  // Dropout scales are folded into the tables that feed the dropped tensors:
+  // Z0 = (W0 · ik0)[type] and gP1 = keep·relu' · (gZ1 (W1 · ik1)ᵀ).
   for (int i = tid; i < (d_in + 1) * FH1; i += blockDim.x)
-    sW0[i] = i < d_in * FH1 ? prm[A.oW0 + i] * A.ik0 * A.ik1 : 0.f;
+    sW0[i] = i < d_in * FH1 ? prm[A.oW0 + i] * A.ik0 : 0.f;
   for (int i = tid; i < D * FK * 12; i += blockDim.x) {
     const int x = i / (FK * 12), rem = i - x * FK * 12, k = rem / 12, y = rem - k * 12;
     sWa[i] = y < D ? prm[A.oW + (x * D + y) * FK + k] : 0.f;
@@ -194,7 +191,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   for (int i = tid; i < FH1 * FH2; i += blockDim.x) {
     const float w = prm[A.oW1 + i];
     sW1[(i / FH2) * W1S + i % FH2] = w * A.ik1;
-    sW1T[(i % FH2) * W1TS + i / FH2] = w * A.ik2;
+    sW1T[(i % FH2) * W1TS + i / FH2] = w;
   }
   for (int i = l; i < 2 * 16 * TS1; i += 64) sT[i] = 0.f;
   if (l < 48) sX[l] = 0.f;
@@ -205,11 +202,10 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   // ik1 · W1[16t+j][4g+q] (gD1 = gZ1 W1ᵀ), contiguous in their tables
   const float *w1bp = sW1T + j * W1TS + 8 * g;
   const float *w1tp = sW1 + j * W1S + 4 * g;
-  const float b0v0 = prm[A.ob0 + j] * A.ik1, b0v1 = prm[A.ob0 + 16 + j] * A.ik1;
-  const float b1v = prm[A.ob1 + j] * A.ik2;
-  const float wdv = prm[A.oWd + j];           // backward: dL/dD2 = gp · Wd
-  const float wdv4 = wdv * A.ik4;             // forward: zpre' = D2 · Wd·ik4 + bd·ik4
-  const float bd4 = prm[A.obd] * A.ik4;
+  const float b0v0 = prm[A.ob0 + j], b0v1 = prm[A.ob0 + 16 + j];
+  const float b1v = prm[A.ob1 + j];
+  const float wdv = prm[A.oWd + j];
+  const float bd = prm[A.obd];
   // NTN lane role: k = j (valid < FK); rows a = 4r + g, r < 3 (valid < D)
   const bool kv = j < FK;
   const int kc = kv ? j : FK - 1;
@@ -390,7 +386,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
               float *T = sT + s * 16 * TS1 + (4 * g + r) * TS1 + 16 * t + j;
               if (r < (s ? K1 : K0)) {
                 const uint32_t d = s ? (h >> 16) : (h & 0xFFFFu);
-                const float v = fmaxf(p1[s][t][r], 0.f);   // P1' = ik1·P1
+                const float v = fmaxf(p1[s][t][r] * A.ik1, 0.f);
                 *T = d < A.thr1 ? v : 0.f;
               } else {
                 *T = 0.f;
@@ -452,11 +448,11 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           for (int s = 0; s < 2; ++s) {
             if (r < (s ? K1 : K0)) {
               const bool k2 = (s ? (h >> 16) : (h & 0xFFFFu)) < A.thr2;
-              d2[s][r] = k2 ? h2[s][r] : 0.f;   // H2' = ik2·H2
+              d2[s][r] = k2 ? h2[s][r] * A.ik2 : 0.f;
               kb |= (k2 ? 1u : 0u) << (3 * s + r);
-              const float z = row_sum16(d2[s][r] * wdv4) + bd4;   // ik4·zpre
+              const float z = row_sum16(d2[s][r] * wdv) + bd;
               const bool k4 = (km4 >> (16 * s + 4 * r)) & 1u;   // includes n < Ns
-              xo[s][r] = ((z > 0.f) & k4) ? z : 0.f;
+              xo[s][r] = ((z > 0.f) & k4) ? z * A.ik4 : 0.f;
             } else {
               d2[s][r] = 0.f;
               xo[s][r] = 0.f;
