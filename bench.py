@@ -27,8 +27,8 @@ FP32_PEAK_TFLOPS = 157.3       # gfx950 fp32 peak (vector = f32 MFMA), MI355X_MI
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
-    p.add_argument('--steps', type=int, default=20)
-    p.add_argument('--warmup', type=int, default=3)
+    p.add_argument('--steps', type=int, default=50)
+    p.add_argument('--warmup', type=int, default=10)
     p.add_argument('--dataset', default='syn_aids700nef')
     p.add_argument('--dropout', type=float, default=0.1)
     p.add_argument('--records', choices=('f32', 'bf16'), default='f32',

@@ -11,6 +11,9 @@ cd "$ROOT"
 timeout -k 10 600 python -m pytest tests -q -m gpu > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest_gpu rc=$rc" | tee -a "$OUT/summary.txt"
 [ $rc -le 1 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$OUT/smoke.log" 2>&1
+rc=$?; echo "smoke rc=$rc" | tee -a "$OUT/summary.txt"
+[ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --json-out "$OUT/bench.json" > "$OUT/bench.log" 2>&1
 rc=$?; echo "bench rc=$rc" | tee -a "$OUT/summary.txt"
 [ $rc -eq 0 ] || exit $rc
