@@ -44,6 +44,31 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
 
 // DPP lane move with bound_ctrl (no "old" operand to materialise), so the
 // compiler can fold it into the consuming VALU op (v_add_f32_dpp).
+// ---- split-bf16 gW0 product ---------------------------------------------------
+// v_mfma_f32_16x16x4_f32 runs on the vector FP32 datapath (it never overlaps VALU
+// on gfx950, scripts/mfma_coexec.hip).  The one-hot operand of gW0 = Xᵀ·gZ0 is
+// exact in bf16, so gZ0 is carried as x = h + m + l (three RNE bf16 parts, each
+// residual exact in f32, |l| <= 2^-16 |x|) and the product runs on
+// v_mfma_f32_16x16x32_bf16: 1.0 × part is exact, accumulation is f32.
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {   // v_cvt_pk_bf16_f32 (RNE)
+  const bf2v v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+// (x0, x1) -> packed bf16 pairs of the h, m, l parts (x = h + m + l)
+__device__ __forceinline__ void split3(float x0, float x1, uint32_t &h, uint32_t &m, uint32_t &l) {
+  h = pk_bf16(x0, x1);
+  const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xFFFF0000u);
+  m = pk_bf16(r0, r1);
+  l = pk_bf16(r0 - __uint_as_float(m << 16), r1 - __uint_as_float(m & 0xFFFF0000u));
+}
+__device__ __forceinline__ f4 mfbf(uint4 a, uint4 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a),
+                                                  __builtin_bit_cast(bf8, b), c, 0, 0, 0);
+}
+
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL,
@@ -618,13 +643,20 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int KS = s ? K1 : K0;
-        // one-hot Xᵀ rows for gW0: k-step q ↔ node 4q + g, row i = j ↔ type 16τ + j
-        float xo0[3], xo1[3];
+        // one-hot Xᵀ for gW0 as a bf16 A operand: row i = j ↔ type 16τ + j, k-slot
+        // 8g + e ↔ node row 4g + (e & 3) (both halves: parts h | m of gZ0)
+        uint4 ohA[2], ohL[2];
 #pragma unroll
-        for (int q = 0; q < KS; ++q) {
-          const int tq = (int)((tys[s] >> (6 * q)) & 63u);
-          xo0[q] = tq == j ? 1.f : 0.f;
-          xo1[q] = tq == 16 + j ? 1.f : 0.f;
+        for (int tau = 0; tau < 2; ++tau) {
+          uint32_t o[3];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            const uint32_t tq = (tys[s] >> (6 * q)) & 63u;
+            o[q] = (q < KS && tq == (uint32_t)(16 * tau + j)) ? 0x3F80u : 0u;   // bf16 1.0
+          }
+          const uint32_t o01 = o[0] | (o[1] << 16), o23 = o[2];
+          ohA[tau] = uint4{o01, o23, o01, o23};
+          ohL[tau] = uint4{o01, o23, 0u, 0u};
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -639,10 +671,16 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           f4 gz0 = {0.f, 0.f, 0.f, 0.f};  // gZ0 = Âᵀ gP1
 #pragma unroll
           for (int q = 0; q < KS; ++q) gz0 = mfma4(af[s][q], gp1[q], gz0);
+          // gW0 / ik0 += Xᵀ gZ0: B k-slots 8g + e = (h | m) parts of node rows 4g + e,
+          // then the l parts (rows 4g+3 of gZ0 are always zero)
+          uint32_t h01, m01, l01, h23 = 0u, m23 = 0u, l23 = 0u;
+          split3(gz0[0], gz0[1], h01, m01, l01);
+          if (KS > 2) split3(gz0[2], 0.f, h23, m23, l23);
+          const uint4 bhm = {h01, h23, m01, m23}, bl = {l01, l23, 0u, 0u};
 #pragma unroll
-          for (int q = 0; q < KS; ++q) {  // gW0 / ik0 += Xᵀ gZ0
-            gw0[0][t] = mfma4(xo0[q], gz0[q], gw0[0][t]);
-            gw0[1][t] = mfma4(xo1[q], gz0[q], gw0[1][t]);
+          for (int tau = 0; tau < 2; ++tau) {
+            gw0[tau][t] = mfbf(ohL[tau], bl, gw0[tau][t]);
+            gw0[tau][t] = mfbf(ohA[tau], bhm, gw0[tau][t]);
           }
         }
       }
