@@ -36,6 +36,8 @@ def parse():
     p.add_argument('--cpu-sample', type=int, default=0,
                    help='pairs for the CPU baseline (0 = auto, -1 = skip)')
     p.add_argument('--json-out', default='')
+    p.add_argument('--emulate-world', type=int, default=0,
+                   help='diagnostic: time rank 0\'s share of a W-GPU step on one GPU (no collective)')
     return p.parse_args()
 
 
@@ -75,7 +77,10 @@ def main():
     gs = load_graph_set(args.dataset, n_max=10)
     labels = gs.label_matrix(flags.yeta)
     model = SiameseGCNTNMSE(gs.d_in, flags, device=device, n_max=gs.n_max)
-    shard = AllPairsShard(gs, labels, rank, world, device=device, dtype=args.records)
+    if args.emulate_world > 1 and world == 1:
+        shard = AllPairsShard(gs, labels, 0, args.emulate_world, device=device, dtype=args.records)
+    else:
+        shard = AllPairsShard(gs, labels, rank, world, device=device, dtype=args.records)
     batch = shard.batch(model)
     hook = make_allreduce_hook() if world > 1 else None
     model.workspace(batch.n_pairs)
@@ -119,6 +124,8 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     total_pairs = shard.total
     value = total_pairs * args.steps / elapsed
+    if args.emulate_world > 1 and world == 1:
+        value = shard.n * args.steps / elapsed   # diagnostic: one emulated rank's own rate
     loss = float(model.loss_buf[0].item() + model.reg_buf[0].item())
 
     if rank == 0:

@@ -296,7 +296,24 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
                  : uint4{0u, 0u, 0u, 0u};
   }
 
-  for (; p < A.n_pairs; p += stride) {
+  // Waves w and w ^ 4 share a SIMD (round-robin placement).  Issue arbitration
+  // favours the older wave, which would finish its pairs far ahead and leave the
+  // younger one alone on the SIMD for the last ~third of the launch.  The higher
+  // priority alternates between the two by pair count (SG_PRIO_PERIOD pairs, the
+  // younger wave holding it in SG_PRIO_YOUNG of them); ties still favour the
+  // older wave.  The pair → wave assignment is unchanged.
+#ifndef SG_PRIO_PERIOD
+#define SG_PRIO_PERIOD 3
+#endif
+#ifndef SG_PRIO_YOUNG
+#define SG_PRIO_YOUNG 2
+#endif
+  int it = 0;
+  const bool young = wv >= 4;
+  for (; p < A.n_pairs; p += stride, ++it) {
+    const bool yturn = (it % SG_PRIO_PERIOD) < SG_PRIO_YOUNG;
+    if (yturn == young) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
     sg_wsync();
     if (A.rec_bf16) {
 #pragma unroll
