@@ -35,6 +35,8 @@ def parse():
                    help='storage of Â in the pair records (bf16 = config C3); math is fp32')
     p.add_argument('--cpu-sample', type=int, default=0,
                    help='pairs for the CPU baseline (0 = auto, -1 = skip)')
+    p.add_argument('--order', choices=('class', 'batch'), default='class',
+                   help='record processing order: class-balanced (sg_pair_order) or batch order')
     p.add_argument('--json-out', default='')
     p.add_argument('--emulate-world', type=int, default=0,
                    help='diagnostic: time rank 0\'s share of a W-GPU step on one GPU (no collective)')
@@ -81,7 +83,7 @@ def main():
         shard = AllPairsShard(gs, labels, 0, args.emulate_world, device=device, dtype=args.records)
     else:
         shard = AllPairsShard(gs, labels, rank, world, device=device, dtype=args.records)
-    batch = shard.batch(model)
+    batch = shard.batch(model, balance=(args.order == 'class'))
     hook = make_allreduce_hook() if world > 1 else None
     model.workspace(batch.n_pairs)
     stream = torch.cuda.current_stream()
@@ -167,6 +169,7 @@ def main():
                        'global_batch': total_pairs, 'n_max': gs.n_max, 'd_in': gs.d_in,
                        'kernel_path': 'fused' if model.kernel_path == 1 else 'generic',
                        'records': '{} Â, {} B/pair'.format(args.records, bytes_pair),
+                       'order': args.order,
                        'parallelism': 'dp{}'.format(world)},
             'roofline': {'bound': 'mfma', 'achieved': achieved_tf, 'peak': FP32_PEAK_TFLOPS,
                          'unit': 'TFLOP/s', 'frac': achieved_tf / FP32_PEAK_TFLOPS,

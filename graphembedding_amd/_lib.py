@@ -82,6 +82,15 @@ def lib():
     L.sg_forward.restype = c_i32
     L.sg_fwd_bwd.argtypes = [pm, vp, c_i64, c_i64, c_i64, vp, c_u64, vp, c_i32, vp, vp, vp, vp, vp]
     L.sg_fwd_bwd.restype = c_i32
+    L.sg_forward_ex.argtypes = [pm, vp, vp, c_i64, c_i64, vp, c_u64, vp, vp, vp]
+    L.sg_forward_ex.restype = c_i32
+    L.sg_fwd_bwd_ex.argtypes = [pm, vp, vp, c_i64, c_i64, c_i64, vp, c_u64, vp, c_i32, vp, vp,
+                                vp, vp, vp]
+    L.sg_fwd_bwd_ex.restype = c_i32
+    L.sg_pair_order_workspace_bytes.argtypes = [pm, c_i64]
+    L.sg_pair_order_workspace_bytes.restype = c_i64
+    L.sg_pair_order.argtypes = [pm, vp, c_i64, vp, vp, vp]
+    L.sg_pair_order.restype = c_i32
     L.sg_adam_tf.argtypes = [vp, vp, vp, vp, c_i64, c_f, c_f, c_f, c_f, c_f, vp, vp, vp]
     L.sg_adam_tf.restype = c_i32
     _lib = L
@@ -90,7 +99,9 @@ def lib():
 
 EXPORTED_SYMBOLS = ('sg_version', 'sg_record_bytes', 'sg_record_bytes_ex', 'sg_model_validate',
                     'sg_workspace_bytes', 'sg_pack_pairs', 'sg_pack_pairs_ex', 'sg_label_stats',
-                    'sg_label_stats_ex', 'sg_forward', 'sg_fwd_bwd', 'sg_adam_tf')
+                    'sg_label_stats_ex', 'sg_forward', 'sg_fwd_bwd', 'sg_adam_tf',
+                    'sg_forward_ex', 'sg_fwd_bwd_ex', 'sg_pair_order',
+                    'sg_pair_order_workspace_bytes')
 
 # sg_dtype: storage type of Â in the pair records
 DTYPES = {'f32': 0, 'bf16': 1}
@@ -213,19 +224,33 @@ def label_stats(records, n_pairs, n_max, stats_out, workspace, stream=None, dtyp
           'sg_label_stats_ex')
 
 
+def pair_order_workspace_bytes(m: SgModel, n_pairs: int) -> int:
+    b = int(lib().sg_pair_order_workspace_bytes(ctypes.byref(m), int(n_pairs)))
+    if b < 0:
+        raise SiameseHipError('sg_pair_order_workspace_bytes: bad arguments')
+    return b
+
+
+def pair_order(m: SgModel, records, n_pairs, order_out, workspace, stream=None):
+    """Class-sorted processing order of the records (include/siamese_hip.h)."""
+    check(lib().sg_pair_order(ctypes.byref(m), _ptr(records), int(n_pairs), _ptr(order_out),
+                              _ptr(workspace), _stream(stream)), 'sg_pair_order')
+
+
 def forward(m: SgModel, records, n_pairs, pair_offset, params, seed, s_out, workspace=None,
-            stream=None):
-    check(lib().sg_forward(ctypes.byref(m), _ptr(records), int(n_pairs), int(pair_offset),
-                           _ptr(params), int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(s_out),
-                           _ptr(workspace), _stream(stream)), 'sg_forward')
+            stream=None, order=None):
+    check(lib().sg_forward_ex(ctypes.byref(m), _ptr(records), _ptr(order), int(n_pairs),
+                              int(pair_offset), _ptr(params), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                              _ptr(s_out), _ptr(workspace), _stream(stream)), 'sg_forward_ex')
 
 
 def fwd_bwd(m: SgModel, records, n_pairs, pair_offset, batch_total, params, seed, y_stats,
-            add_label_term, s_out, grad_out, loss_out, workspace, stream=None):
-    check(lib().sg_fwd_bwd(ctypes.byref(m), _ptr(records), int(n_pairs), int(pair_offset),
-                           int(batch_total), _ptr(params), int(seed) & 0xFFFFFFFFFFFFFFFF,
-                           _ptr(y_stats), int(add_label_term), _ptr(s_out), _ptr(grad_out),
-                           _ptr(loss_out), _ptr(workspace), _stream(stream)), 'sg_fwd_bwd')
+            add_label_term, s_out, grad_out, loss_out, workspace, stream=None, order=None):
+    check(lib().sg_fwd_bwd_ex(ctypes.byref(m), _ptr(records), _ptr(order), int(n_pairs),
+                              int(pair_offset), int(batch_total), _ptr(params),
+                              int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(y_stats), int(add_label_term),
+                              _ptr(s_out), _ptr(grad_out), _ptr(loss_out), _ptr(workspace),
+                              _stream(stream)), 'sg_fwd_bwd_ex')
 
 
 def adam_tf(params, m, v, grad, lr, beta1, beta2, eps, weight_decay, beta_powers, reg_loss=None,

@@ -86,7 +86,8 @@ class AllPairsShard(object):
         self.n = self.end - self.start
         self.record_bytes = 4 * record_words(gs.n_max, dtype)
 
-    def batch(self, model, rank: int = 0):
-        return model.batch_from_records(self.records, self.n, self.labels,
-                                        pair_offset=self.start, batch_total=self.total,
-                                        y_stats=self.y_stats)
+    def batch(self, model, rank: int = 0, balance: bool = True):
+        b = model.batch_from_records(self.records, self.n, self.labels,
+                                     pair_offset=self.start, batch_total=self.total,
+                                     y_stats=self.y_stats)
+        return model.balance(b) if balance else b

@@ -100,6 +100,7 @@ __device__ __forceinline__ float row_sum16(float v) {
 
 struct FastArgs {
   const uint8_t *recs;
+  const int32_t *order;   // processing order (sg_pair_order) or null
   int64_t n_pairs;
   int64_t pair_offset;
   int rw4h;      // 16-B words per HBM record (f32 or bf16 Â)
@@ -172,8 +173,24 @@ __device__ __forceinline__ int fast_param(const FastArgs &A, int s, int l) {
   }
 }
 
+#ifdef SG_FAST_TIMING
+// Diagnostic build only (scripts/fast_timing.py): per-wave s_memrealtime stamps
+// (100 MHz) at start / after the prologue / after the pair loop / at the end,
+// plus the wave's pair count.
+constexpr int kTimeWaves = 4096;
+__device__ unsigned long long sg_fast_times[kTimeWaves * 5];
+#define SG_STAMP(slot, val)                                                        \
+  do {                                                                             \
+    const int tw_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);            \
+    if ((threadIdx.x & 63) == 0 && tw_ < kTimeWaves) sg_fast_times[tw_ * 5 + (slot)] = (val); \
+  } while (0)
+#else
+#define SG_STAMP(slot, val) do {} while (0)
+#endif
+
 template <int D, bool BWD, bool ALIGNED, bool INTENDED>
 __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
+  SG_STAMP(0, __builtin_amdgcn_s_memrealtime());
   extern __shared__ __attribute__((aligned(16))) float smem[];
   using L = FastLds<D>;
   constexpr int RW4 = L::RW / 4;
@@ -189,6 +206,45 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   const int d_in = A.d_in;
   const float *__restrict__ prm = A.params;
 
+  // ---- pair schedule; the first record is loaded during the prologue ----
+  // Slots are handed out round by round (round r: slots [r·S, r·S + S), S = all
+  // waves of the grid).  With an order (sg_pair_order: records sorted by cost
+  // class) the waves walk the rounds as a snake (odd rounds reversed), so every
+  // wave gets the same class mix and the launch has no slow tail; slot q then
+  // holds record order[q].  p is the record (= batch pair index) either way.
+  // (32-bit indices: sg_fast_run admits n_pairs < 2^31 - grid)
+  const int npairs = (int)A.n_pairs;
+  const int stride = (int)gridDim.x * nw;
+  const int gw = (int)blockIdx.x * nw + wv;
+  const int32_t *__restrict__ ord = A.order;
+  auto slot_of = [&](int r) -> int {
+    return r * stride + ((ord != nullptr && (r & 1)) ? stride - 1 - gw : gw);
+  };
+  // record indices of 64 rounds, lane i ↔ round r0 + i (read back with readlane)
+  auto load_ord = [&](int r0) -> int {
+    const int s = slot_of(r0 + l);
+    return s < npairs ? ord[s] : 0;
+  };
+  // an entry read back from ordA, clamped (scalar) so a bad order never reads out of bounds
+  auto ord_at = [&](int v, int lane) -> int {
+    const int x = __builtin_amdgcn_readlane(v, lane);
+    return x < 0 ? 0 : (x >= npairs ? npairs - 1 : x);
+  };
+  int ordA = 0, ordB = 0;
+  if (ord) {
+    ordA = load_ord(0);
+    ordB = load_ord(64);
+  }
+  // the parameter staging's loads go out together with the order's
+  float *stg = smem + A.shared_floats;   // fast_cfg sizes LDS for n_params floats here
+  const int nprm = A.n_params, bdx = (int)blockDim.x;
+  float stv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int i = k * bdx + tid;
+    stv[k] = i < nprm ? prm[i] : 0.f;
+  }
+
   float *sW0 = smem;                            // W0 · ik0, row d_in zero
   float *sWa = sW0 + (d_in + 1) * FH1;          // [a][k][12]: W[a][b][k] at b
   float *sWb = sWa + D * FK * 12;               // [b][k][12]: W[a][b][k] at a
@@ -200,45 +256,72 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   float *sT = W + L::TILE;
   float *sX = W + L::X;
 
+  // Prologue.  The raw parameter vector is staged into LDS (in the wave regions,
+  // unused until the pair loop) in one pass with all loads in flight, and the
+  // tables are built from there: one global-load latency instead of one per table.
   // Dropout scales are folded into the tables that feed the dropped tensors:
   // Z0 = (W0 · ik0)[type] and gP1 = keep·relu' · (gZ1 (W1 · ik1)ᵀ).
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int i = k * bdx + tid;
+    if (i < nprm) stg[i] = stv[k];
+  }
+  for (int i = 8 * bdx + tid; i < nprm; i += bdx) stg[i] = prm[i];   // small blocks only
+  // first record: its HBM latency overlaps the table build below
+  int q = slot_of(0);
+  int p = (ord && q < npairs) ? ord_at(ordA, 0) : q;
+  // HBM record: rw4h 16-B words (RW4 for f32 Â, fewer for bf16 Â)
+  const int rw4h = A.rw4h;
+  constexpr int ADJ4 = D * D / 4;   // 16-B words of a bf16 adjacency block (D even)
+  uint4 pre[NREC];
+#pragma unroll
+  for (int c = 0; c < NREC; ++c) {
+    const int w4 = l + 64 * c;
+    pre[c] = (q < npairs && w4 < rw4h)
+                 ? ((const uint4 *)(A.recs + (size_t)p * (size_t)rw4h * 16u))[w4]
+                 : uint4{0u, 0u, 0u, 0u};
+  }
+  __syncthreads();
   for (int i = tid; i < (d_in + 1) * FH1; i += blockDim.x)
-    sW0[i] = i < d_in * FH1 ? prm[A.oW0 + i] * A.ik0 : 0.f;
+    sW0[i] = i < d_in * FH1 ? stg[A.oW0 + i] * A.ik0 : 0.f;
   for (int i = tid; i < D * FK * 12; i += blockDim.x) {
     const int x = i / (FK * 12), rem = i - x * FK * 12, k = rem / 12, y = rem - k * 12;
-    sWa[i] = y < D ? prm[A.oW + (x * D + y) * FK + k] : 0.f;
-    sWb[i] = y < D ? prm[A.oW + (y * D + x) * FK + k] : 0.f;
+    sWa[i] = y < D ? stg[A.oW + (x * D + y) * FK + k] : 0.f;
+    sWb[i] = y < D ? stg[A.oW + (y * D + x) * FK + k] : 0.f;
   }
   for (int i = tid; i < FK * 24; i += blockDim.x) {
     const int k = i / 24, c = i - k * 24;
-    sV[i] = c < 2 * D ? prm[A.oV + k * 2 * D + c] : 0.f;
+    sV[i] = c < 2 * D ? stg[A.oV + k * 2 * D + c] : 0.f;
   }
   for (int i = tid; i < FH1 * FH2; i += blockDim.x) {
-    const float w = prm[A.oW1 + i];
+    const float w = stg[A.oW1 + i];
     sW1[(i / FH2) * W1S + i % FH2] = w * A.ik1;
     sW1T[(i % FH2) * W1TS + i / FH2] = w;
   }
+  // per-lane parameters, also from the staged copy
+  const int j_ = tid & 15;
+  const float b0v0 = stg[A.ob0 + j_], b0v1 = stg[A.ob0 + 16 + j_];
+  const float b1v = stg[A.ob1 + j_];
+  const float wdv = stg[A.oWd + j_];
+  const float bd = stg[A.obd];
+  const bool kv = j_ < FK;
+  const int kc = kv ? j_ : FK - 1;
+  const float Uk = kv ? stg[A.oU + kc] : 0.f;
+  const float bnk = kv ? stg[A.obn + kc] : 0.f;
+  float usum = 0.f;
+#pragma unroll
+  for (int k = 0; k < FK; ++k) usum += stg[A.oU + k];
+  __syncthreads();   // the staging area is dead: the waves take their regions
   for (int i = l; i < 2 * 16 * TS1; i += 64) sT[i] = 0.f;
-  if (l < 48) sX[l] = 0.f;
-  __syncthreads();
+  if (l < 48) sX[l] = 0.f;   // wave-private: the pair loop's first sg_wsync orders it
+  SG_STAMP(1, __builtin_amdgcn_s_memrealtime());
 
   // ---- per-lane constants ----
   // MFMA B fragments of W1 read from LDS at use: W1[8g+q][j] (Z1 = D1 W1) and
   // ik1 · W1[16t+j][4g+q] (gD1 = gZ1 W1ᵀ), contiguous in their tables
   const float *w1bp = sW1T + j * W1TS + 8 * g;
   const float *w1tp = sW1 + j * W1S + 4 * g;
-  const float b0v0 = prm[A.ob0 + j], b0v1 = prm[A.ob0 + 16 + j];
-  const float b1v = prm[A.ob1 + j];
-  const float wdv = prm[A.oWd + j];
-  const float bd = prm[A.obd];
   // NTN lane role: k = j (valid < FK); rows a = 4r + g, r < 3 (valid < D)
-  const bool kv = j < FK;
-  const int kc = kv ? j : FK - 1;
-  const float Uk = kv ? prm[A.oU + kc] : 0.f;
-  const float bnk = kv ? prm[A.obn + kc] : 0.f;
-  float usum = 0.f;
-#pragma unroll
-  for (int k = 0; k < FK; ++k) usum += prm[A.oU + k];
   // A-operand row of this lane: tile row i = j ↔ node ni.  Â is read at static
   // per-lane offsets; entries outside the n_max × n_max block (tile rows and
   // columns past n_max) read the always-zero sX[47].  Entries of absent nodes
@@ -282,20 +365,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   float gbn = 0.f, gUa = 0.f, lossa = 0.f;
   const float ybar = (BWD && !ALIGNED) ? A.y_stats[0] : 0.f;
 
-  const int64_t stride = (int64_t)gridDim.x * nw;
-  int64_t p = (int64_t)blockIdx.x * nw + wv;
-  // HBM record: rw4h 16-B words (RW4 for f32 Â, fewer for bf16 Â)
-  const int rw4h = A.rw4h;
-  constexpr int ADJ4 = D * D / 4;   // 16-B words of a bf16 adjacency block (D even)
-  uint4 pre[NREC];
-#pragma unroll
-  for (int c = 0; c < NREC; ++c) {
-    const int w4 = l + 64 * c;
-    pre[c] = (p < A.n_pairs && w4 < rw4h)
-                 ? ((const uint4 *)(A.recs + (size_t)p * (size_t)rw4h * 16u))[w4]
-                 : uint4{0u, 0u, 0u, 0u};
-  }
-
   // Waves w and w ^ 4 share a SIMD (round-robin placement).  Issue arbitration
   // favours the older wave, which would finish its pairs far ahead and leave the
   // younger one alone on the SIMD for the last ~third of the launch.  The higher
@@ -310,7 +379,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #endif
   int it = 0;
   const bool young = wv >= 4;
-  for (; p < A.n_pairs; p += stride, ++it) {
+  for (; q < npairs; ++it) {
     const bool yturn = (it % SG_PRIO_PERIOD) < SG_PRIO_YOUNG;
     if (yturn == young) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
@@ -339,14 +408,26 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       }
     }
     sg_wsync();
+    const int pcur = p;
     {
-      const int64_t pn = p + stride;
+      const int qn = slot_of(it + 1);
+      int pn = qn;
+      if (ord) {
+        const int rl = (it + 1) & 63;
+        if (rl == 0) {
+          ordA = ordB;
+          ordB = load_ord(it + 65);
+        }
+        pn = qn < npairs ? ord_at(ordA, rl) : 0;
+      }
 #pragma unroll
       for (int c = 0; c < NREC; ++c) {
         const int w4 = l + 64 * c;
-        if (pn < A.n_pairs && w4 < rw4h)
+        if (qn < npairs && w4 < rw4h)
           pre[c] = ((const uint4 *)(A.recs + (size_t)pn * (size_t)rw4h * 16u))[w4];
       }
+      q = qn;
+      p = pn;
     }
     const int *ty = (const int *)sRec;
     // wave-uniform node counts (clamped to n_max)
@@ -354,7 +435,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
     int N1 = __builtin_amdgcn_readfirstlane(((const int *)sRec)[2 * D * D + 2 * D + 1]);
     N0 = N0 < 0 ? 0 : (N0 > D ? D : N0);
     N1 = N1 < 0 ? 0 : (N1 > D ? D : N1);
-    const uint32_t pk = sg_pair_key(A.key, (uint32_t)(A.pair_offset + p));
+    const uint32_t pk = sg_pair_key(A.key, (uint32_t)(A.pair_offset + pcur));
 
     // ---- layer-0 (node) and NTN-input dropout masks: one hash per lane, two ballots ----
     // lanes 0..15: layer 0, node e = l; lanes 16..31: layer 4, element e = l - 16.
@@ -545,10 +626,10 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       const float rsum = row_sum16(rk);
       const float sv = INTENDED ? row_sum16(Uk * rk) : usum * rsum;
       if (!BWD) {
-        if (l == 0) A.s_out[p] = sv;
+        if (l == 0) A.s_out[pcur] = sv;
         return;
       }
-      if (A.s_out && l == 0) A.s_out[p] = sv;
+      if (A.s_out && l == 0) A.s_out[pcur] = sv;
       const float yhat = __expf(-A.yeta * sv * sv);   // v_exp_f32: ~1e-7 relative
       float gy;
       if (!ALIGNED) {
@@ -712,6 +793,8 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
     }
   }
 
+  SG_STAMP(2, __builtin_amdgcn_s_memrealtime());
+  SG_STAMP(4, (unsigned long long)it);
   if (!BWD) return;
   // ---- flush: every wave dumps its accumulator slots to LDS, all threads sum ----
   // Slot s of lane (g, j) maps to at most one parameter (fast_param below) and
@@ -768,6 +851,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
     for (int w = 0; w < nw; ++w) acc += F[(size_t)w * NS * 64 + idx];
     dst[prm_i] = acc;
   }
+  SG_STAMP(3, __builtin_amdgcn_s_memrealtime());
 }
 
 struct FastCfg {
@@ -779,7 +863,7 @@ struct FastCfg {
 };
 
 template <int D>
-FastCfg fast_cfg_t(int d_in, int64_t n_pairs, bool bwd) {
+FastCfg fast_cfg_t(int d_in, int n_params, int64_t n_pairs, bool bwd) {
   FastCfg c;
   c.D = D;
   c.shared_floats = FastLds<D>::shared_floats(d_in);
@@ -813,8 +897,11 @@ FastCfg fast_cfg_t(int d_in, int64_t n_pairs, bool bwd) {
   if (per_cu < 1) per_cu = 1;
   // the flush dumps every wave's accumulator slots into the block's LDS
   const size_t fl = bwd ? (size_t)best * FlushSlots<D>::NS * 64u * 4u : 0u;
-  if (fl > c.lds) {
-    c.lds = fl;
+  // the prologue stages the parameter vector behind the shared tables
+  const size_t stage = (size_t)(c.shared_floats + n_params) * 4u;
+  const size_t need = fl > stage ? fl : stage;
+  if (need > c.lds) {
+    c.lds = need;
     per_cu = (int)(163840u / c.lds);
   }
   const int64_t want = (n_pairs + best - 1) / best;
@@ -854,12 +941,13 @@ int sg_fast_supported(const sg_model_t *m, const SgGenPlan &P) {
   return fast_shape(m, P) ? 1 : 0;
 }
 
-static FastCfg fast_cfg(int D, int d_in, int64_t n_pairs, bool bwd) {
-  return D == 12 ? fast_cfg_t<12>(d_in, n_pairs, bwd) : fast_cfg_t<10>(d_in, n_pairs, bwd);
+static FastCfg fast_cfg(const SgGenPlan &P, int64_t n_pairs, bool bwd) {
+  return P.n_max == 12 ? fast_cfg_t<12>(P.d_in, P.n_params, n_pairs, bwd)
+                       : fast_cfg_t<10>(P.d_in, P.n_params, n_pairs, bwd);
 }
 
 int64_t sg_fast_slab_floats(const SgGenPlan &P, int64_t n_pairs) {
-  FastCfg c = fast_cfg(P.n_max, P.d_in, n_pairs, true);
+  FastCfg c = fast_cfg(P, n_pairs, true);
   return (int64_t)c.blocks * (P.n_params + 1);
 }
 
@@ -888,13 +976,16 @@ static void launch_fast(const FastCfg &c, bool bwd, bool aligned, bool intended,
 }
 
 int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
-                int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
+                const int32_t *order, int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
                 uint64_t seed, const float *y_stats, float *s_out, float *slab, int *blocks_out,
                 hipStream_t stream) {
   const int D = P.n_max;
-  FastCfg c = fast_cfg(D, P.d_in, n_pairs, bwd);
+  FastCfg c = fast_cfg(P, n_pairs, bwd);
+  // the kernel indexes pairs in 32 bits (2^31 records would be ≥ 1 TB)
+  if (n_pairs > 0x7FFFFFFF - (int64_t)c.blocks * c.waves * 2) return SG_ERR_ARG;
   FastArgs A;
   A.recs = (const uint8_t *)recs;
+  A.order = order;
   A.n_pairs = n_pairs;
   A.rw4h = P.hbm_words / 4;
   A.rec_bf16 = P.adj_dtype == SG_DTYPE_BF16 ? 1 : 0;
@@ -938,3 +1029,11 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
   if (blocks_out) *blocks_out = c.blocks;
   return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
 }
+
+#ifdef SG_FAST_TIMING
+extern "C" int sg_fast_timing_fetch(unsigned long long *host, int n) {
+  if (n > kTimeWaves * 5) n = kTimeWaves * 5;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(sg_fast_times), (size_t)n * 8u, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? n : -1;
+}
+#endif

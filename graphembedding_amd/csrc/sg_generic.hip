@@ -15,6 +15,7 @@ namespace {
 
 struct GenArgs {
   const uint8_t *recs;
+  const int32_t *order;   // processing order (sg_pair_order) or null
   int64_t n_pairs;
   int64_t pair_offset;
   float inv_batch;      // 1/B for the aligned loss
@@ -327,7 +328,12 @@ __global__ void __launch_bounds__(256) sg_generic_kernel(SgGenPlan P, GenArgs A)
   const int nmax = P.n_max;
   const float ybar = (BWD && P.loss_mode == SG_LOSS_BROADCAST) ? A.y_stats[0] : 0.f;
   float loss_acc = 0.f;
-  for (int64_t p = (int64_t)blockIdx.x * nw + wave; p < A.n_pairs; p += (int64_t)gridDim.x * nw) {
+  for (int64_t q = (int64_t)blockIdx.x * nw + wave; q < A.n_pairs; q += (int64_t)gridDim.x * nw) {
+    int64_t p = q;   // record = batch pair index
+    if (A.order) {
+      const int v = A.order[q];
+      p = v < 0 ? 0 : (v >= A.n_pairs ? A.n_pairs - 1 : v);   // never out of bounds
+    }
     const uint32_t *rec = (const uint32_t *)(A.recs + (size_t)p * (size_t)P.hbm_words * 4u);
     uint32_t *R = (uint32_t *)(S + P.l_rec);
     if (P.adj_dtype == SG_DTYPE_BF16) {   // widen Â to the f32 LDS layout
@@ -507,14 +513,15 @@ int64_t sg_generic_slab_floats(const SgGenPlan &P, int64_t n_pairs) {
   return (int64_t)L.blocks * (P.n_params + 1);
 }
 
-int sg_generic_run(const SgGenPlan &P, bool bwd, const void *recs, int64_t n_pairs,
-                   int64_t pair_offset, int64_t batch_total, const float *params, uint64_t seed,
+int sg_generic_run(const SgGenPlan &P, bool bwd, const void *recs, const int32_t *order,
+                   int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params, uint64_t seed,
                    const float *y_stats, float *s_out, float *slab, int *blocks_out,
                    hipStream_t stream) {
   SgGenLaunch L = sg_generic_launch(P, n_pairs, bwd);
   if (L.lds_bytes > 163840u) return SG_ERR_UNSUPPORTED;
   GenArgs A;
   A.recs = (const uint8_t *)recs;
+  A.order = order;
   A.n_pairs = n_pairs;
   A.pair_offset = pair_offset;
   A.inv_batch = batch_total > 0 ? 1.f / (float)batch_total : 0.f;

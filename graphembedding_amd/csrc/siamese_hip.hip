@@ -25,15 +25,15 @@ int sg_num_cus() {
 // generic path (sg_generic.hip)
 int sg_generic_lds_ok(const SgGenPlan &P, bool bwd);
 int64_t sg_generic_slab_floats(const SgGenPlan &P, int64_t n_pairs);
-int sg_generic_run(const SgGenPlan &P, bool bwd, const void *recs, int64_t n_pairs,
-                   int64_t pair_offset, int64_t batch_total, const float *params, uint64_t seed,
+int sg_generic_run(const SgGenPlan &P, bool bwd, const void *recs, const int32_t *order,
+                   int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params, uint64_t seed,
                    const float *y_stats, float *s_out, float *slab, int *blocks_out,
                    hipStream_t stream);
 // fused fast path (sg_fast.hip)
 int sg_fast_supported(const sg_model_t *m, const SgGenPlan &P);
 int64_t sg_fast_slab_floats(const SgGenPlan &P, int64_t n_pairs);
 int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
-                int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
+                const int32_t *order, int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
                 uint64_t seed, const float *y_stats, float *s_out, float *slab, int *blocks_out,
                 hipStream_t stream);
 
@@ -69,19 +69,22 @@ __global__ void __launch_bounds__(1024) sg_reduce_one(const float *__restrict__ 
   __shared__ float red[16][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + lane;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  // wave w sums rows w + 16 k in a fixed order; 16 rows per batch with every load
+  // in flight (one memory latency per 256 slab rows)
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
   if (col < C) {
     const float *p = slab + col;
     int b = w;
-    for (; b + 48 < nblk; b += 64) {
-      a0 += p[(size_t)b * C];
-      a1 += p[(size_t)(b + 16) * C];
-      a2 += p[(size_t)(b + 32) * C];
-      a3 += p[(size_t)(b + 48) * C];
+    for (; b + 16 * 15 < nblk; b += 256) {
+      float v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = p[(size_t)(b + 16 * k) * C];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) a[k & 3] += v[k];
     }
-    for (; b < nblk; b += 16) a0 += p[(size_t)b * C];
+    for (; b < nblk; b += 16) a[0] += p[(size_t)b * C];
   }
-  red[w][lane] = (a0 + a1) + (a2 + a3);
+  red[w][lane] = (a[0] + a[1]) + (a[2] + a[3]);
   __syncthreads();
   if (w == 0 && col < C) {
     float v = 0.f;
@@ -203,6 +206,103 @@ __global__ void __launch_bounds__(256) sg_pack_kernel(const float *__restrict__ 
   }
 }
 
+// ---- processing order: stable counting sort of the records by cost class ----
+// Key of a record = the cost class of its pair in the kernel that will run it:
+// fused path (N0 > 8) + (N1 > 8) (third Â k-step per side, and the shared-tile
+// PACK body when both sides fit 8 nodes); generic path N0 + N1.  Blocks own
+// contiguous chunks; counts are stored key-major so one exclusive scan gives
+// every (key, chunk) its output base; the scatter keeps record order within a
+// key (ballot ranks), so the permutation is deterministic.
+constexpr int kOrderChunk = 8192;   // records per block
+constexpr int kOrderKeys = 129;     // 2·n_max + 1 keys at n_max ≤ 64
+
+__device__ __forceinline__ int sg_order_key(const uint8_t *__restrict__ recs, int64_t p,
+                                            int rec_words, int n_off, int nmax, int fast) {
+  const int32_t *r = (const int32_t *)(recs + (size_t)p * (size_t)rec_words * 4u) + n_off;
+  int n0 = r[0], n1 = r[1];
+  n0 = n0 < 0 ? 0 : (n0 > nmax ? nmax : n0);
+  n1 = n1 < 0 ? 0 : (n1 > nmax ? nmax : n1);
+  return fast ? (n0 > 8) + (n1 > 8) : n0 + n1;
+}
+
+__global__ void __launch_bounds__(256) sg_order_count(const uint8_t *__restrict__ recs, int64_t n,
+                                                      int rec_words, int n_off, int nmax,
+                                                      int fast, int K, int nb,
+                                                      int32_t *__restrict__ cnt) {
+  __shared__ int h[kOrderKeys];
+  for (int k = threadIdx.x; k < K; k += blockDim.x) h[k] = 0;
+  __syncthreads();
+  const int64_t b0 = (int64_t)blockIdx.x * kOrderChunk;
+  for (int i = threadIdx.x; i < kOrderChunk && b0 + i < n; i += blockDim.x)
+    atomicAdd(&h[sg_order_key(recs, b0 + i, rec_words, n_off, nmax, fast)], 1);
+  __syncthreads();
+  for (int k = threadIdx.x; k < K; k += blockDim.x) cnt[(size_t)k * nb + blockIdx.x] = h[k];
+}
+
+// in-place exclusive scan of m ints, one workgroup (m = K · chunks: small)
+__global__ void __launch_bounds__(1024) sg_order_scan(int32_t *__restrict__ a, int64_t m) {
+  __shared__ int s[1024];
+  __shared__ int carry;
+  const int t = threadIdx.x;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (int64_t c0 = 0; c0 < m; c0 += 1024) {
+    const int v = c0 + t < m ? a[c0 + t] : 0;
+    s[t] = v;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+      const int u = t >= d ? s[t - d] : 0;
+      __syncthreads();
+      s[t] += u;
+      __syncthreads();
+    }
+    const int base = carry;
+    if (c0 + t < m) a[c0 + t] = base + s[t] - v;
+    __syncthreads();
+    if (t == 1023) carry = base + s[1023];
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(256) sg_order_scatter(const uint8_t *__restrict__ recs, int64_t n,
+                                                        int rec_words, int n_off, int nmax,
+                                                        int fast, int K, int nb,
+                                                        const int32_t *__restrict__ base,
+                                                        int32_t *__restrict__ order) {
+  __shared__ int run[kOrderKeys];
+  __shared__ int wc[4][kOrderKeys];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  for (int k = t; k < K; k += blockDim.x) run[k] = base[(size_t)k * nb + blockIdx.x];
+  const int64_t b0 = (int64_t)blockIdx.x * kOrderChunk;
+  const int64_t b1 = b0 + kOrderChunk < n ? b0 + kOrderChunk : n;
+  for (int64_t t0 = b0; t0 < b1; t0 += 256) {
+    for (int i = t; i < 4 * kOrderKeys; i += blockDim.x) (&wc[0][0])[i] = 0;
+    __syncthreads();
+    const int64_t p = t0 + t;
+    const bool valid = p < b1;
+    const int key = valid ? sg_order_key(recs, p, rec_words, n_off, nmax, fast) : -1;
+    // rank among the earlier lanes of this wave with the same key
+    int rank = 0;
+    uint64_t active = __ballot(valid);
+    while (active) {
+      const int k = __builtin_amdgcn_readlane(key, __builtin_ctzll(active));
+      const uint64_t m = __ballot(valid && key == k);
+      if (key == k) rank = __popcll(m & ((1ull << lane) - 1ull));
+      if (lane == 0) wc[w][k] = __popcll(m);
+      active &= ~m;
+    }
+    __syncthreads();
+    if (valid) {
+      int off = run[key] + rank;
+      for (int v = 0; v < w; ++v) off += wc[v][key];
+      order[off] = (int32_t)p;
+    }
+    __syncthreads();
+    for (int k = t; k < K; k += blockDim.x) run[k] += wc[0][k] + wc[1][k] + wc[2][k] + wc[3][k];
+    __syncthreads();
+  }
+}
+
 // ---- TF ApplyAdam (+ weight decay gradient) in one workgroup ----
 __global__ void __launch_bounds__(1024) sg_adam_kernel(float *__restrict__ th, float *__restrict__ m,
                                                        float *__restrict__ v,
@@ -210,27 +310,46 @@ __global__ void __launch_bounds__(1024) sg_adam_kernel(float *__restrict__ th, f
                                                        float lr, float b1, float b2, float eps,
                                                        float wd, float *__restrict__ bp,
                                                        float *__restrict__ reg_loss) {
-  __shared__ double red[1024];
+  __shared__ double red[16];
   const float b1p = bp[0], b2p = bp[1];
   const float alpha = lr * sqrtf(1.f - b2p) / (1.f - b1p);
   const float c1 = 1.f - b1, c2 = 1.f - b2;
+  const int t = threadIdx.x;
   double reg = 0.0;
-  for (int64_t i = threadIdx.x; i < n; i += 1024) {
-    const float t = th[i];
-    reg += (double)t * (double)t;
-    const float gi = g[i] + wd * t;
-    const float mi = m[i] + (gi - m[i]) * c1;
-    const float vi = v[i] + (gi * gi - v[i]) * c2;
-    m[i] = mi;
-    v[i] = vi;
-    th[i] = t - (mi * alpha) / (sqrtf(vi) + eps);
+  // 4 parameters per thread per pass, all loads issued before any update
+  for (int64_t base = 0; base < n; base += 4096) {
+    float tv[4], gv[4], mv[4], vv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t i = base + k * 1024 + t;
+      if (i < n) {
+        tv[k] = th[i];
+        gv[k] = g[i];
+        mv[k] = m[i];
+        vv[k] = v[i];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t i = base + k * 1024 + t;
+      if (i < n) {
+        reg += (double)tv[k] * (double)tv[k];
+        const float gi = gv[k] + wd * tv[k];
+        const float mi = mv[k] + (gi - mv[k]) * c1;
+        const float vi = vv[k] + (gi * gi - vv[k]) * c2;
+        m[i] = mi;
+        v[i] = vi;
+        th[i] = tv[k] - (mi * alpha) / (sqrtf(vi) + eps);
+      }
+    }
   }
-  red[threadIdx.x] = reg;
+  // Σθ²: butterfly within each wave, then the 16 wave sums in order (deterministic)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) reg += __shfl_xor(reg, o);
+  if ((t & 63) == 0) red[t >> 6] = reg;
   __syncthreads();
-  for (int o = 512; o > 0; o >>= 1) {
-    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
-  }
+  if (t == 0)
+    for (int w = 1; w < 16; ++w) red[0] += red[w];
   if (threadIdx.x == 0) {
     bp[0] = b1p * b1;
     bp[1] = b2p * b2;
@@ -278,7 +397,7 @@ PathChoice choose_path(const sg_model_t *m, bool bwd) {
 // ===========================================================================
 extern "C" {
 
-int32_t sg_version(void) { return 10100; }   /* 1.1.0: bf16 Â records */
+int32_t sg_version(void) { return 10200; }   /* 1.2.0: pair processing order */
 
 int64_t sg_record_bytes(int32_t n_max) { return sg_record_bytes_ex(n_max, SG_DTYPE_F32); }
 
@@ -366,19 +485,56 @@ int32_t sg_label_stats_ex(const void *records, int64_t n_pairs, int32_t n_max, i
   return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
 }
 
+int64_t sg_pair_order_workspace_bytes(const sg_model_t *model, int64_t n_pairs) {
+  if (!model || n_pairs < 0) return -1;
+  const int64_t nb = (n_pairs + kOrderChunk - 1) / kOrderChunk;
+  return nb * kOrderKeys * 4 + 256;
+}
+
+int32_t sg_pair_order(const sg_model_t *model, const void *records, int64_t n_pairs,
+                      int32_t *order_out, void *workspace, sg_stream_t stream) {
+  if (n_pairs < 0 || n_pairs > 0x7FFFFFFF) return SG_ERR_ARG;
+  if (n_pairs == 0) return SG_OK;
+  if (!records || !order_out || !workspace) return SG_ERR_ARG;
+  PathChoice c = choose_path(model, true);
+  if (c.status != SG_OK) return c.status;
+  const int nmax = c.plan.n_max;
+  const SgRecLayout rl = sg_rec_layout(nmax, c.plan.adj_dtype);
+  const int n_off = rl.adj_words + 2 * nmax;
+  const int fast = c.fast ? 1 : 0;
+  const int K = fast ? 3 : 2 * nmax + 1;
+  const int nb = (int)((n_pairs + kOrderChunk - 1) / kOrderChunk);
+  hipStream_t st = (hipStream_t)stream;
+  int32_t *cnt = (int32_t *)workspace;
+  hipLaunchKernelGGL(sg_order_count, dim3(nb), dim3(256), 0, st, (const uint8_t *)records, n_pairs,
+                     rl.words, n_off, nmax, fast, K, nb, cnt);
+  hipLaunchKernelGGL(sg_order_scan, dim3(1), dim3(1024), 0, st, cnt, (int64_t)K * nb);
+  hipLaunchKernelGGL(sg_order_scatter, dim3(nb), dim3(256), 0, st, (const uint8_t *)records,
+                     n_pairs, rl.words, n_off, nmax, fast, K, nb, (const int32_t *)cnt, order_out);
+  return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
+}
+
 int32_t sg_forward(const sg_model_t *model, const void *records, int64_t n_pairs,
                    int64_t pair_offset, const float *params, uint64_t seed, float *s_out,
                    void *workspace, sg_stream_t stream) {
+  return sg_forward_ex(model, records, nullptr, n_pairs, pair_offset, params, seed, s_out,
+                       workspace, stream);
+}
+
+int32_t sg_forward_ex(const sg_model_t *model, const void *records, const int32_t *order,
+                      int64_t n_pairs, int64_t pair_offset, const float *params, uint64_t seed,
+                      float *s_out, void *workspace, sg_stream_t stream) {
   (void)workspace;
   if (n_pairs < 0 || pair_offset < 0) return SG_ERR_ARG;
+  if (order && n_pairs > 0x7FFFFFFF) return SG_ERR_ARG;
   if (n_pairs == 0) return SG_OK;
   if (!records || !params || !s_out) return SG_ERR_ARG;
   PathChoice c = choose_path(model, false);
   if (c.status != SG_OK) return c.status;
   if (c.fast)
-    return sg_fast_run(model, c.plan, false, records, n_pairs, pair_offset, n_pairs, params, seed,
-                       nullptr, s_out, nullptr, nullptr, (hipStream_t)stream);
-  return sg_generic_run(c.plan, false, records, n_pairs, pair_offset, n_pairs, params, seed,
+    return sg_fast_run(model, c.plan, false, records, order, n_pairs, pair_offset, n_pairs, params,
+                       seed, nullptr, s_out, nullptr, nullptr, (hipStream_t)stream);
+  return sg_generic_run(c.plan, false, records, order, n_pairs, pair_offset, n_pairs, params, seed,
                         nullptr, s_out, nullptr, nullptr, (hipStream_t)stream);
 }
 
@@ -386,7 +542,17 @@ int32_t sg_fwd_bwd(const sg_model_t *model, const void *records, int64_t n_pairs
                    int64_t pair_offset, int64_t batch_total, const float *params, uint64_t seed,
                    const float *y_stats, int32_t add_label_term, float *s_out, float *grad_out,
                    float *loss_out, void *workspace, sg_stream_t stream) {
+  return sg_fwd_bwd_ex(model, records, nullptr, n_pairs, pair_offset, batch_total, params, seed,
+                       y_stats, add_label_term, s_out, grad_out, loss_out, workspace, stream);
+}
+
+int32_t sg_fwd_bwd_ex(const sg_model_t *model, const void *records, const int32_t *order,
+                      int64_t n_pairs, int64_t pair_offset, int64_t batch_total,
+                      const float *params, uint64_t seed, const float *y_stats,
+                      int32_t add_label_term, float *s_out, float *grad_out, float *loss_out,
+                      void *workspace, sg_stream_t stream) {
   if (n_pairs < 0 || pair_offset < 0) return SG_ERR_ARG;
+  if (order && n_pairs > 0x7FFFFFFF) return SG_ERR_ARG;
   if (!params || !grad_out || !workspace) return SG_ERR_ARG;
   PathChoice c = choose_path(model, true);
   if (c.status != SG_OK) return c.status;
@@ -405,11 +571,11 @@ int32_t sg_fwd_bwd(const sg_model_t *model, const void *records, int64_t n_pairs
   int nblk = 0;
   int rc;
   if (c.fast)
-    rc = sg_fast_run(model, c.plan, true, records, n_pairs, pair_offset, batch_total, params, seed,
-                     y_stats, s_out, slab, &nblk, st);
+    rc = sg_fast_run(model, c.plan, true, records, order, n_pairs, pair_offset, batch_total,
+                     params, seed, y_stats, s_out, slab, &nblk, st);
   else
-    rc = sg_generic_run(c.plan, true, records, n_pairs, pair_offset, batch_total, params, seed,
-                        y_stats, s_out, slab, &nblk, st);
+    rc = sg_generic_run(c.plan, true, records, order, n_pairs, pair_offset, batch_total, params,
+                        seed, y_stats, s_out, slab, &nblk, st);
   if (rc != SG_OK) return rc;
   float *part = slab + (size_t)nblk * C;
   return launch_reduce(slab, nblk, C, part, grad_out, loss_out, y_stats,

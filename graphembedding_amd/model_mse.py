@@ -72,6 +72,7 @@ class Batch:
     pair_offset: int = 0            # global index of record 0 (dropout RNG / sharding)
     batch_total: int = 0            # global batch size B
     gid_pairs: Optional[np.ndarray] = None
+    order: object = None            # torch.int32 [n] processing order (balance()) or None
 
 
 class SiameseGCNTNMSE(object):
@@ -126,7 +127,7 @@ class SiameseGCNTNMSE(object):
         torch = self.torch
         s = torch.empty(batch.n_pairs, dtype=torch.float32, device=self.device)
         _lib.forward(self.sg, batch.records, batch.n_pairs, batch.pair_offset, self.params,
-                     self._seed(seed), s)
+                     self._seed(seed), s, order=batch.order)
         return s
 
     def get_feed_dict(self, data, dist_calculator, tvt, test_id=None, train_id=None):
@@ -213,7 +214,23 @@ class SiameseGCNTNMSE(object):
         _lib.fwd_bwd(self.sg, batch.records, batch.n_pairs, batch.pair_offset,
                      batch.batch_total, self.params, self._seed(seed), batch.y_stats,
                      1 if add_label_term else 0, s_out, self.grad, self.loss_buf,
-                     self.workspace(batch.n_pairs))
+                     self.workspace(batch.n_pairs), order=batch.order)
+
+    def balance(self, batch: Batch) -> Batch:
+        """Attach the class-sorted processing order of the batch's records
+        (sg_pair_order): every wavefront then gets the same mix of cheap and
+        expensive pairs.  Scores are unchanged; the gradient differs only by
+        summation order.  Worth it for batches that are stepped repeatedly
+        (all-pairs epochs), not for the reference's B = 5 feeds."""
+        torch = self.torch
+        if batch.n_pairs == 0:
+            return batch
+        ws = torch.empty(_lib.pair_order_workspace_bytes(self.sg, batch.n_pairs) // 4 + 1,
+                         dtype=torch.int32, device=self.device)
+        order = torch.empty(batch.n_pairs, dtype=torch.int32, device=self.device)
+        _lib.pair_order(self.sg, batch.records, batch.n_pairs, order, ws)
+        batch.order = order
+        return batch
 
     def apply_adam(self):
         f = self.flags

@@ -199,6 +199,31 @@ int32_t sg_fwd_bwd(const sg_model_t *model, const void *records, int64_t n_pairs
                    float *loss_out, void *workspace, sg_stream_t stream);
 
 /*
+ * Processing order (library 1.2).  The per-pair cost of the kernels depends on
+ * the pair's node counts; records in batch order hand every wavefront a random
+ * mix, so the launch waits for the unluckiest one.  sg_pair_order writes a
+ * permutation of [0, n_pairs) that sorts the records by cost class (stable, so
+ * deterministic); sg_forward_ex / sg_fwd_bwd_ex walk it so that every wavefront
+ * gets the same mix.  Results are those of the unordered call up to the
+ * summation order of the gradient: record i still keys its dropout masks by
+ * pair_offset + i and writes s_out[i].  Compute the order once per packed
+ * batch and reuse it for every step.  order == NULL is batch order.
+ * Entries outside [0, n_pairs) are clamped (never read out of bounds), but
+ * only a permutation gives the batch's result.
+ */
+int64_t sg_pair_order_workspace_bytes(const sg_model_t *model, int64_t n_pairs);
+int32_t sg_pair_order(const sg_model_t *model, const void *records, int64_t n_pairs,
+                      int32_t *order_out, void *workspace, sg_stream_t stream);
+int32_t sg_forward_ex(const sg_model_t *model, const void *records, const int32_t *order,
+                      int64_t n_pairs, int64_t pair_offset, const float *params, uint64_t seed,
+                      float *s_out, void *workspace, sg_stream_t stream);
+int32_t sg_fwd_bwd_ex(const sg_model_t *model, const void *records, const int32_t *order,
+                      int64_t n_pairs, int64_t pair_offset, int64_t batch_total,
+                      const float *params, uint64_t seed, const float *y_stats,
+                      int32_t add_label_term, float *s_out, float *grad_out, float *loss_out,
+                      void *workspace, sg_stream_t stream);
+
+/*
  * TF ApplyAdam (training_ops ApplyAdam, non-Nesterov) with the weight-decay
  * gradient wd·θ added first (models.py:69-73):
  *   g = grad + wd·θ; α = lr·√(1-β2^t)/(1-β1^t); m += (g-m)(1-β1);
