@@ -10,13 +10,17 @@
 // k-ordered fmaf chain.  Node n lives in tile row ρ(n) = 4·(n%4) + n/4, so the
 // accumulator of one product (lane (g,j) holds rows 4g..4g+3) IS the B operand
 // of the next Â product with the K index permuted (k-step κ ↔ rows 4g+κ), and
-// rows 4g+3 are empty for n ≤ 12: Â products need 3 k-steps, not 4.  The
+// rows 4g+3 are empty for n ≤ 12: Â products need 3 k-steps, not 4 (2 for
+// sides of ≤ 8 nodes: the pair body is instantiated per (K0, K1) class, and
+// pairs of two ≤ 8-node sides share one tile in the feature products).  The
 // feature-contracting products need one 16×32 / 16×16 transpose through LDS.
-// The NTN head runs on VALU (D = K = 10 is too small for MFMA to pay), lanes
-// (ag, k) = (l/10, l%10) own NTN weight rows a ∈ {ag, ag+6}.
-// Parameter gradients accumulate in registers (gW1 in MFMA accumulators) and a
-// per-wave LDS table (gW0 rows, scattered by node type), flushed once per
-// launch, wave by wave, into one slab row per workgroup (deterministic).
+// The one-hot gW0 = Xᵀ·gZ0 product runs on bf16 MFMA with gZ0 split in three
+// bf16 parts (one-hot is exact in bf16).  The NTN head runs on VALU (D = K = 10
+// is too small for MFMA to pay): lanes (g, k = j) own NTN weight rows
+// a ∈ {g, g+4, g+8}, the tiles' node map; cross-row sums use DPP and permlanes.
+// Parameter gradients accumulate in registers (gW1, gW0 in MFMA accumulators),
+// are flushed once per launch through LDS, waves summed in a fixed order, into
+// one slab row per workgroup (deterministic).
 #include <type_traits>
 
 #include "sg_plan.h"
