@@ -70,6 +70,7 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     device = torch.device('cuda', local)
 
+    from graphembedding_amd import _lib
     from graphembedding_amd.allpairs import AllPairsShard, load_graph_set
     from graphembedding_amd.config import Flags
     from graphembedding_amd.model_mse import SiameseGCNTNMSE
@@ -167,7 +168,7 @@ def main():
             'config': {'workload': 'AIDS700nef all-pairs (700 graphs, 490,000 ordered pairs), '
                                    'default 5-layer Siamese GCN-NTN, dropout {}'.format(args.dropout),
                        'global_batch': total_pairs, 'n_max': gs.n_max, 'd_in': gs.d_in,
-                       'kernel_path': 'fused' if model.kernel_path == 1 else 'generic',
+                       'kernel_path': _lib.PATH_NAMES[model.kernel_path],
                        'records': '{} Â, {} B/pair'.format(args.records, bytes_pair),
                        'order': args.order,
                        'parallelism': 'dp{}'.format(world)},

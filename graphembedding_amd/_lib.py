@@ -97,6 +97,8 @@ def lib():
     return L
 
 
+PATH_NAMES = {0: 'generic', 1: 'fused', 2: 'fused32'}
+
 EXPORTED_SYMBOLS = ('sg_version', 'sg_record_bytes', 'sg_record_bytes_ex', 'sg_model_validate',
                     'sg_workspace_bytes', 'sg_pack_pairs', 'sg_pack_pairs_ex', 'sg_label_stats',
                     'sg_label_stats_ex', 'sg_forward', 'sg_fwd_bwd', 'sg_adam_tf',
@@ -178,7 +180,8 @@ def make_model(layers: List[dict], d_in: int, n_max: int, keep_prob: float, fina
 
 
 def validate(m: SgModel):
-    """Returns (n_params, path) where path 1 = fused fast kernel, 0 = generic."""
+    """Returns (n_params, path): path 1 = fused kernel (sg_fast), 2 = fused capacity-32
+    kernel (sg_fast32, config C4), 0 = generic kernel."""
     n = ctypes.c_int64(0)
     p = ctypes.c_int32(0)
     check(lib().sg_model_validate(ctypes.byref(m), ctypes.byref(n), ctypes.byref(p)),

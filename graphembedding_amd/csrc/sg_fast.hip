@@ -24,12 +24,13 @@
 #include <type_traits>
 
 #include "sg_plan.h"
+#include "sg_mfma.h"
 
 int sg_num_cus();
 
 namespace {
 
-typedef float f4 __attribute__((ext_vector_type(4)));
+using namespace sgk;
 
 constexpr int FH1 = 32, FH2 = 16, FK = 10;
 constexpr int TS1 = 36;  // D1 tile row stride (floats)
@@ -41,66 +42,6 @@ constexpr int W1TS = 36; // W1ᵀ table row stride (32 + pad)
 #endif
 // waves per block: 8 = 2 waves per SIMD at up to 256 VGPRs per lane
 constexpr int MAXW = SG_FAST_MAXW;
-
-__device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-// DPP lane move with bound_ctrl (no "old" operand to materialise), so the
-// compiler can fold it into the consuming VALU op (v_add_f32_dpp).
-// ---- split-bf16 gW0 product ---------------------------------------------------
-// v_mfma_f32_16x16x4_f32 runs on the vector FP32 datapath (it never overlaps VALU
-// on gfx950, scripts/mfma_coexec.hip).  The one-hot operand of gW0 = Xᵀ·gZ0 is
-// exact in bf16, so gZ0 is carried as x = h + m + l (three RNE bf16 parts, each
-// residual exact in f32, |l| <= 2^-16 |x|) and the product runs on
-// v_mfma_f32_16x16x32_bf16: 1.0 × part is exact, accumulation is f32.
-typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {   // v_cvt_pk_bf16_f32 (RNE)
-  const bf2v v = {(__bf16)a, (__bf16)b};
-  return __builtin_bit_cast(uint32_t, v);
-}
-// (x0, x1) -> packed bf16 pairs of the h, m, l parts (x = h + m + l)
-__device__ __forceinline__ void split3(float x0, float x1, uint32_t &h, uint32_t &m, uint32_t &l) {
-  h = pk_bf16(x0, x1);
-  const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xFFFF0000u);
-  m = pk_bf16(r0, r1);
-  l = pk_bf16(r0 - __uint_as_float(m << 16), r1 - __uint_as_float(m & 0xFFFF0000u));
-}
-__device__ __forceinline__ f4 mfbf(uint4 a, uint4 b, f4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a),
-                                                  __builtin_bit_cast(bf8, b), c, 0, 0, 0);
-}
-
-template <int CTRL>
-__device__ __forceinline__ float dpp(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL,
-                                                            0xF, 0xF, true));
-}
-
-
-// x[l] + x[l ^ 16] and x[l] + x[l ^ 32]: gfx950 v_permlane16/32_swap leave x[l]
-// and its partner in the two registers (either order), one add completes the sum
-__device__ __forceinline__ float xsum16(float x) {
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false,
-                                                  false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ float xsum32(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false,
-                                                  false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-
-// Sum over the 16 lanes of a DPP row; result in every lane of the row.
-__device__ __forceinline__ float row_sum16(float v) {
-  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp<0x141>(v);  // row_half_mirror
-  v += dpp<0x140>(v);  // row_mirror
-  return v;
-}
 
 struct FastArgs {
   const uint8_t *recs;

@@ -1,0 +1,871 @@
+// sg_fast32.hip — fused fwd(+bwd) kernel for the reference's default Siamese
+// stack at node capacity 32: config C4 (AIDS10knef, N <= 30, Padding/NTN
+// input_dim D in (12, 32]; config.py:44-66 with max_in_dims = input_dim = D).
+//
+// Same scheme as sg_fast.hip (one wavefront per pair, f32 MFMA for every GCN
+// product, masks folded into data), for graphs of up to 32 nodes:
+//  * each graph is two 16-row tiles; node n sits in tile n/16, row
+//    ρ(n % 16) = 4·(n%4) + (n%16)/4, so an accumulator is the B operand of the next
+//    Â product and node-contracting products run over the ceil(N/4) k-blocks of
+//    4 nodes that hold nodes (runtime trip counts: N is 5..30 in C4);
+//  * records are stored at capacity 32 (Â row stride 32), so the whole 32×32
+//    block can be read without bounds checks (zero beyond N: record contract);
+//  * the NTN head (D up to 32) runs on VALU from one LDS table Wa[a][k][b]:
+//    ge2 = Σ_a x1[a] W[a][b][k] gm[k] is formed as per-lane partials over the
+//    lane's rows a and reduce-scattered across the four row groups with
+//    v_permlane32/16_swap (no transposed copy of W in LDS);
+//  * the NTN weight gradient Σ_pairs gm[k] x1[a] x2[b] (D·D·K = 9,000 entries)
+//    does not fit per-lane registers, so each pair writes (x1 | 1, x2 | 1, gm) to
+//    a buffer and sg_ntn_wgrad_kernel computes Σ gm ⊗ (x1|1) ⊗ (x2|1) with MFMA:
+//    gW, and through the constant entries gV and the NTN bias gradient too
+//    (split over the same workgroups, written into the same slab rows: the
+//    reduction is unchanged).  Hence D <= 31 (slot D holds the 1).
+#include <type_traits>
+
+#include "sg_mfma.h"
+#include "sg_plan.h"
+
+int sg_num_cus();
+
+namespace {
+using namespace sgk;
+
+constexpr int FH1 = 32, FH2 = 16, FK = 10;
+constexpr int NC = 32;     // record node capacity
+constexpr int TS1 = 36;    // D1 transpose tile row stride
+constexpr int W1S = 20;    // W1·ik1 [32][16] row stride
+constexpr int W1TS = 36;   // W1ᵀ [16][32] row stride
+constexpr int WAS = 32;    // Wa[a][k][b] row stride (b)
+constexpr int VS = 64;     // V[k][c] row stride (c < 2D)
+constexpr int NBUF = 80;   // NTN buffer floats per pair: x1[32] | x2[32] | gm[16]
+constexpr int MAXW = 8;    // waves per block (2 per SIMD)
+
+struct F32Args {
+  const uint8_t *recs;
+  const int32_t *order;
+  int64_t n_pairs;
+  int64_t pair_offset;
+  int rw4h;       // 16-B words per HBM record
+  int rec_bf16;
+  const float *params;
+  const float *y_stats;
+  float *s_out;
+  float *slab;
+  float *ntn;     // [n_pairs][NBUF] (backward)
+  uint32_t key;
+  uint32_t thr0, thr1, thr2, thr4;
+  float ik0, ik1, ik2, ik4;
+  float yeta, inv_batch;
+  int d_in, n_params, D;
+  int shared_floats, wave_floats;
+  int oW0, ob0, oW1, ob1, oWd, obd, oW, oV, oU, obn;
+};
+
+// per-wave LDS (floats): record image | D1 transpose tile (one side) | x1 | x2 | pad
+struct Lds32 {
+  static constexpr int RW = 2 * NC * NC + 2 * NC + 4;   // 2116 record words
+  static constexpr int REC = 0;
+  static constexpr int TILE = 2120;
+  static constexpr int X = TILE + 2 * 16 * TS1;          // x1[32] | x2[32]
+  static constexpr int WAVE = X + 72;
+  static int shared_floats(int d_in, int D) {
+    return (d_in + 1) * FH1 + D * FK * WAS + FK * VS + FH1 * W1S + FH2 * W1TS;
+  }
+};
+
+// flush slots of one lane: gW1 (8) | gW0/ik0 (16) | dU, loss | db0 (2), db1, dWd, dbd
+// (the NTN W, V and bias gradients come from sg_ntn_wgrad_kernel)
+constexpr int NS32 = 8 + 16 + 2 + 5;
+
+__device__ __forceinline__ int f32_param(const F32Args &A, int s, int l) {
+  const int g = l >> 4, j = l & 15;
+  if (s < 8) return A.oW1 + (16 * (s >> 2) + 4 * g + (s & 3)) * FH2 + j;
+  s -= 8;
+  if (s < 16) {
+    const int ty = 16 * (s >> 3) + 4 * g + (s & 3);
+    return ty < A.d_in ? A.oW0 + ty * FH1 + 16 * ((s >> 2) & 1) + j : -1;
+  }
+  s -= 16;
+  switch (s) {
+    case 0: return (g == 0 && j < FK) ? A.oU + j : -1;
+    case 1: return l == 0 ? A.n_params : -1;
+    case 2: return g == 0 ? A.ob0 + j : -1;
+    case 3: return g == 0 ? A.ob0 + 16 + j : -1;
+    case 4: return g == 0 ? A.ob1 + j : -1;
+    case 5: return g == 0 ? A.oWd + j : -1;
+    case 6: return l == 0 ? A.obd : -1;
+    default: return -1;
+  }
+}
+
+template <bool BWD, bool ALIGNED, bool INTENDED>
+__global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  using L = Lds32;
+  constexpr int RW4 = L::RW / 4;   // 529
+  const int tid = threadIdx.x;
+  const int l = tid & 63, nw = blockDim.x >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = l >> 4, j = l & 15;
+  const uint32_t lb1 = (uint32_t)(FH1 * g + j);   // layer 1: e = 32 n + f
+  const uint32_t lb2 = (uint32_t)(FH2 * g + j);   // layer 2: e = 16 n + j
+  const int d_in = A.d_in, D = A.D;
+  const float *__restrict__ prm = A.params;
+
+  // ---- parameter staging (behind the shared tables) and tables ----
+  float *sW0 = smem;                            // W0 · ik0, row d_in zero
+  float *sWa = sW0 + (d_in + 1) * FH1;          // [a][k][WAS]: W[a][b][k] at b
+  float *sV = sWa + D * FK * WAS;               // [k][VS]
+  float *sW1 = sV + FK * VS;                    // W1 · ik1 [32][W1S]
+  float *sW1T = sW1 + FH1 * W1S;                // W1ᵀ [16][W1TS]
+  float *stg = smem + A.shared_floats;
+  {
+    const int n = A.n_params, bdx = (int)blockDim.x;
+    for (int b = 0; b < n; b += 8 * bdx) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i = b + k * bdx + tid;
+        v[k] = i < n ? prm[i] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i = b + k * bdx + tid;
+        if (i < n) stg[i] = v[k];
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < (d_in + 1) * FH1; i += blockDim.x)
+    sW0[i] = i < d_in * FH1 ? stg[A.oW0 + i] * A.ik0 : 0.f;
+  for (int i = tid; i < D * FK * WAS; i += blockDim.x) {
+    const int a = i / (FK * WAS), rem = i - a * FK * WAS, k = rem / WAS, b = rem - k * WAS;
+    sWa[i] = b < D ? stg[A.oW + (a * D + b) * FK + k] : 0.f;
+  }
+  for (int i = tid; i < FK * VS; i += blockDim.x) {
+    const int k = i / VS, c = i - k * VS;
+    sV[i] = c < 2 * D ? stg[A.oV + k * 2 * D + c] : 0.f;
+  }
+  for (int i = tid; i < FH1 * FH2; i += blockDim.x) {
+    const float w = stg[A.oW1 + i];
+    sW1[(i / FH2) * W1S + i % FH2] = w * A.ik1;
+    sW1T[(i % FH2) * W1TS + i / FH2] = w;
+  }
+  const float b0v0 = stg[A.ob0 + j], b0v1 = stg[A.ob0 + 16 + j];
+  const float b1v = stg[A.ob1 + j];
+  const float wdv = stg[A.oWd + j];
+  const float bd = stg[A.obd];
+  const bool kv = j < FK;
+  const int kc = kv ? j : FK - 1;
+  const float Uk = kv ? stg[A.oU + kc] : 0.f;
+  const float bnk = kv ? stg[A.obn + kc] : 0.f;
+  float usum = 0.f;
+#pragma unroll
+  for (int k = 0; k < FK; ++k) usum += stg[A.oU + k];
+  __syncthreads();   // staging area dead: the waves take their regions
+  float *W = smem + A.shared_floats + wv * A.wave_floats;
+  float *sRec = W + L::REC;
+  float *sT = W + L::TILE;
+  float *sX = W + L::X;
+  for (int i = l; i < 72; i += 64) sX[i] = 0.f;
+
+  // per-lane constants: A row of this lane in an Â product = node(to, j) =
+  // 16 to + 4 (j % 4) + j / 4, k column 4 b + g (record row stride NC)
+  const int ni = 4 * (j & 3) + (j >> 2);
+  const int abase0 = L::REC + ni * NC + g;   // + s·NC² + 16·NC·to + 4 b
+  const float *w1bp = sW1T + j * W1TS + 8 * g;   // W1[8g+q][j] (Z1 = D1 W1)
+  const float *w1tp = sW1 + j * W1S + 4 * g;     // ik1·W1[16t+j][4g+q] (gD1)
+
+  // ---- accumulators ----
+  f4 gw1[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+  f4 gw0[2][2] = {{f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}},
+                  {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}}};
+  float gb0a0 = 0.f, gb0a1 = 0.f, gb1a = 0.f, gwda = 0.f, gbda = 0.f;
+  float gUa = 0.f, lossa = 0.f;
+  const float ybar = (BWD && !ALIGNED) ? A.y_stats[0] : 0.f;
+
+  // ---- schedule (as sg_fast: snake over the waves when an order is given) ----
+  const int npairs = (int)A.n_pairs;
+  const int stride = (int)gridDim.x * nw;
+  const int gw = (int)blockIdx.x * nw + wv;
+  const int32_t *__restrict__ ord = A.order;
+  auto slot_of = [&](int r) -> int {
+    return r * stride + ((ord != nullptr && (r & 1)) ? stride - 1 - gw : gw);
+  };
+  const int rw4h = A.rw4h;
+  constexpr int ADJ4 = NC * NC / 4;   // 16-B words of a bf16 adjacency block
+
+  for (int it = 0;; ++it) {
+    const int q = slot_of(it);
+    if (q >= npairs) break;
+    int p = q;
+    if (ord) {
+      const int v = ord[q];
+      p = v < 0 ? 0 : (v >= npairs ? npairs - 1 : v);
+    }
+    // ---- stage the record (f32 LDS image; bf16 Â widened) ----
+    {
+      const uint4 *src = (const uint4 *)(A.recs + (size_t)(uint32_t)p * (size_t)rw4h * 16u);
+      constexpr int NREC = (RW4 + 63) / 64;
+      uint4 v[NREC];
+#pragma unroll
+      for (int c = 0; c < NREC; ++c) {
+        const int w4 = l + 64 * c;
+        v[c] = w4 < rw4h ? src[w4] : uint4{0u, 0u, 0u, 0u};
+      }
+      sg_wsync();   // the previous pair's LDS reads are done
+      if (A.rec_bf16) {
+#pragma unroll
+        for (int c = 0; c < NREC; ++c) {
+          const int w4 = l + 64 * c;
+          if (w4 < ADJ4) {
+            const uint4 x = v[c];
+            f4 lo = {__uint_as_float(x.x << 16), __uint_as_float(x.x & 0xFFFF0000u),
+                     __uint_as_float(x.y << 16), __uint_as_float(x.y & 0xFFFF0000u)};
+            f4 hi = {__uint_as_float(x.z << 16), __uint_as_float(x.z & 0xFFFF0000u),
+                     __uint_as_float(x.w << 16), __uint_as_float(x.w & 0xFFFF0000u)};
+            ((f4 *)sRec)[2 * w4] = lo;
+            ((f4 *)sRec)[2 * w4 + 1] = hi;
+          } else if (w4 < rw4h) {
+            ((uint4 *)sRec)[w4 + ADJ4] = v[c];
+          }
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < NREC; ++c) {
+          const int w4 = l + 64 * c;
+          if (w4 < RW4) ((uint4 *)sRec)[w4] = v[c];
+        }
+      }
+      sg_wsync();
+    }
+    const int *ty = (const int *)sRec + 2 * NC * NC;
+    int N0 = __builtin_amdgcn_readfirstlane(ty[2 * NC]);
+    int N1 = __builtin_amdgcn_readfirstlane(ty[2 * NC + 1]);
+    N0 = N0 < 0 ? 0 : (N0 > D ? D : N0);
+    N1 = N1 < 0 ? 0 : (N1 > D ? D : N1);
+    const int KB0 = (N0 + 3) >> 2, KB1 = (N1 + 3) >> 2;   // k-blocks of 4 nodes
+    const int T0 = N0 > 16 ? 2 : 1, T1 = N1 > 16 ? 2 : 1;
+    const int KBm = KB0 > KB1 ? KB0 : KB1;
+    const uint32_t pk = sg_pair_key(A.key, (uint32_t)(A.pair_offset + p));
+    const float label = sRec[2 * NC * NC + 2 * NC + 2];
+
+    // ---- layer-0 (node) and NTN-input dropout masks: one hash per lane ----
+    // lanes 0..31: layer 0, node e = l; lanes 32..63: layer 4, element e = l - 32
+    uint32_t km0[2], km4[2];   // bit n ↔ node / element n of side s (0 when n >= N_s)
+    {
+      const int e = l & 31;
+      const bool hi = l >= 32;
+      const uint32_t h = sg_hash(pk, hi ? 4u : 0u, (uint32_t)e);
+      const uint32_t thr = hi ? A.thr4 : A.thr0;
+      const uint64_t b0 = __ballot((e < N0) & ((h & 0xFFFFu) < thr));
+      const uint64_t b1 = __ballot((e < N1) & ((h >> 16) < thr));
+      km0[0] = (uint32_t)b0;
+      km4[0] = (uint32_t)(b0 >> 32);
+      km0[1] = (uint32_t)b1;
+      km4[1] = (uint32_t)(b1 >> 32);
+    }
+
+    // Â A-fragments of side s: Â[node(to, j)][4b + g] for the side's tiles / k-blocks,
+    // re-read from the record image (intact for the whole pair) in each phase
+    auto load_af = [&](int s, int T, int KB, float (&af)[2][8]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const int ab = abase0 + s * NC * NC + 4 * b;
+        af[0][b] = b < KB ? W[ab] : 0.f;
+        af[1][b] = (b < KB && T > 1) ? W[ab + 16 * NC] : 0.f;
+      }
+    };
+
+    // ================= forward: P1 = Â Z0 + b0 =================
+    uint32_t tyA[2][2];     // [s][tile]: types of node rows 4g+r, 6 bits; 63 = dropped/absent
+    f4 d1[2][2][2];         // [s][to][f]: P1, then D1 in place
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int KB = s ? KB1 : KB0, T = s ? T1 : T0;
+      const uint32_t kms = km0[s];
+      uint32_t tp[2] = {0u, 0u};
+#pragma unroll
+      for (int to = 0; to < 2; ++to) {
+        d1[s][to][0] = f4{b0v0, b0v0, b0v0, b0v0};
+        d1[s][to][1] = f4{b0v1, b0v1, b0v1, b0v1};
+      }
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        if (b < KB) {
+          const int n = 4 * b + g;
+          uint32_t t_ = (uint32_t)ty[s * NC + n];
+          t_ = min(t_, (uint32_t)(d_in - 1));
+          const uint32_t k0 = (kms >> n) & 1u;
+          tp[b >> 2] |= (k0 ? t_ : 63u) << (6 * (b & 3));
+          const float *w0 = sW0 + (k0 ? t_ : (uint32_t)d_in) * FH1 + j;
+          const float z0a = w0[0], z0b = w0[16];
+          const int ab = abase0 + s * NC * NC + 4 * b;
+          const float a0 = W[ab];
+          d1[s][0][0] = mfma4(a0, z0a, d1[s][0][0]);
+          d1[s][0][1] = mfma4(a0, z0b, d1[s][0][1]);
+          if (T > 1) {
+            const float a1 = W[ab + 16 * NC];
+            d1[s][1][0] = mfma4(a1, z0a, d1[s][1][0]);
+            d1[s][1][1] = mfma4(a1, z0b, d1[s][1][1]);
+          }
+        } else {
+          tp[b >> 2] |= 63u << (6 * (b & 3));
+        }
+      }
+      tyA[s][0] = tp[0];
+      tyA[s][1] = tp[1];
+    }
+    // D1 = dropout(relu(P1)): one hash per element (node 16to+4r+g, feature 16f+j)
+    // gives both sides' draws; k-blocks past a side's nodes are zeroed
+#pragma unroll
+    for (int to = 0; to < 2; ++to)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int nb = 4 * to + r;
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          if (nb < KBm) {
+            const uint32_t h =
+                sg_mix((pk ^ ((1u << 26) | (uint32_t)(512 * to + 128 * r + 16 * f))) ^ lb1);
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              const uint32_t dr = s ? (h >> 16) : (h & 0xFFFFu);
+              const float v = fmaxf(d1[s][to][f][r] * A.ik1, 0.f);
+              d1[s][to][f][r] = (nb < (s ? KB1 : KB0) && dr < A.thr1) ? v : 0.f;
+            }
+          } else {
+            d1[0][to][f][r] = d1[1][to][f][r] = 0.f;
+          }
+        }
+      }
+
+    // Z1 = D1 W1 (D1 transposed through the tile), H2 = Â Z1 + b1, per side
+    f4 h2[2][2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int KB = s ? KB1 : KB0, T = s ? T1 : T0;
+#pragma unroll
+      for (int to = 0; to < 2; ++to) {
+        if (to < T) {
+#pragma unroll
+          for (int f = 0; f < 2; ++f)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sT[(16 * to + 4 * g + r) * TS1 + 16 * f + j] = d1[s][to][f][r];
+        }
+      }
+      sg_wsync();
+      f4 z1[2];
+      const f4 wlo = *(const f4 *)w1bp, whi = *(const f4 *)(w1bp + 4);
+#pragma unroll
+      for (int to = 0; to < 2; ++to) {
+        z1[to] = f4{0.f, 0.f, 0.f, 0.f};
+        if (to < T) {
+          const float *Tr = sT + (16 * to + j) * TS1 + 8 * g;
+          const f4 lo = *(const f4 *)Tr, hi = *(const f4 *)(Tr + 4);
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) z1[to] = mfma4(lo[qq], wlo[qq], z1[to]);
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) z1[to] = mfma4(hi[qq], whi[qq], z1[to]);
+        }
+      }
+      float af[2][8];
+      load_af(s, T, KB, af);
+#pragma unroll
+      for (int to = 0; to < 2; ++to) {
+        h2[s][to] = f4{b1v, b1v, b1v, b1v};
+        if (to < T) {
+#pragma unroll
+          for (int b = 0; b < 8; ++b)
+            if (b < KB) h2[s][to] = mfma4(af[to][b], z1[b >> 2][b & 3], h2[s][to]);
+        }
+      }
+      sg_wsync();   // the tile is rewritten by the next side
+    }
+
+    // D2 = dropout(H2); zpre = D2·Wd + bd; x = dropout(pad(relu(zpre)))
+    float xo[2][8], d2[2][8];   // [s][4 to + r] ↔ node 16 to + 4 r + g
+    uint32_t kb2[2] = {0u, 0u};
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) {
+      const int to = nb >> 2, r = nb & 3;
+      if (nb < KBm) {
+        const uint32_t h = sg_mix((pk ^ ((2u << 26) | (uint32_t)(256 * to + 64 * r))) ^ lb2);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          if (nb < (s ? KB1 : KB0)) {
+            const bool k2 = (s ? (h >> 16) : (h & 0xFFFFu)) < A.thr2;
+            d2[s][nb] = k2 ? h2[s][to][r] * A.ik2 : 0.f;
+            kb2[s] |= (k2 ? 1u : 0u) << nb;
+            const float z = row_sum16(d2[s][nb] * wdv) + bd;
+            const bool k4 = (km4[s] >> (16 * to + 4 * r + g)) & 1u;   // includes n < N
+            xo[s][nb] = ((z > 0.f) & k4) ? z * A.ik4 : 0.f;
+          } else {
+            d2[s][nb] = xo[s][nb] = 0.f;
+          }
+        }
+      } else {
+        d2[0][nb] = d2[1][nb] = xo[0][nb] = xo[1][nb] = 0.f;
+      }
+    }
+    if (j == 0) {   // x1 | x2 for every lane (node 16to+4r+g of row group g)
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb) {
+        sX[4 * nb + g] = xo[0][nb];
+        sX[NC + 4 * nb + g] = xo[1][nb];
+      }
+    }
+    sg_wsync();
+
+    // ================= NTN head (layers.py:282-310) =================
+    // lane (g, k = j) owns rows a = 4r' + g.  Per 4-column block bq of b (outer loop):
+    // u[r'] += Σ_b W[a][b][k] x2[b] (forward), and the partials Σ_{own a} x1[a] W[a][b][k]
+    // of ge2 = Σ_a x1[a] W[a][b][k] gm[k] share the Wa reads; the partials of the
+    // block are reduce-scattered over the four row groups at once (half 0 = g < 2
+    // keeps b % 4 < 2, then row g keeps b % 4 == g): cs[bq] ↔ b = 4 bq + g.
+    float u[8], cs[8];
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) u[rr] = cs[rr] = 0.f;
+#pragma unroll
+    for (int bq = 0; bq < 8; ++bq) {
+      if (bq < KB1) {
+        const f4 x2 = *(const f4 *)(sX + NC + 4 * bq);
+        float cb[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) {
+          if (rr < KB0) {
+            const int a = 4 * rr + g;
+            const int ac = a < D ? a : 0;
+            const f4 w = *(const f4 *)(sWa + (ac * FK + kc) * WAS + 4 * bq);
+            const float x1a = xo[0][rr];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              u[rr] = fmaf(w[e], x2[e], u[rr]);
+              cb[e] = fmaf(x1a, w[e], cb[e]);
+            }
+          }
+        }
+        float hs[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(cb[e]),
+                                                            __float_as_uint(cb[e + 2]), false, false);
+          hs[e] = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+        }
+        const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(hs[0]),
+                                                          __float_as_uint(hs[1]), false, false);
+        cs[bq] = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+      }
+    }
+    float mpart = 0.f;
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      if (rr < KB0) {
+        const int a = 4 * rr + g;
+        const int ac = a < D ? a : 0;
+        mpart = fmaf(xo[0][rr], u[rr] + sV[kc * VS + ac], mpart);
+      }
+      if (rr < KB1) {
+        const int b = 4 * rr + g;
+        const int bc = b < D ? b : 0;
+        mpart = fmaf(xo[1][rr], sV[kc * VS + D + bc], mpart);
+      }
+    }
+    const float m = xsum32(xsum16(mpart)) + bnk;
+    const float rk = (kv & (m > 0.f)) ? m : 0.f;
+    const float rsum = row_sum16(rk);
+    const float sv = INTENDED ? row_sum16(Uk * rk) : usum * rsum;
+    if (!BWD) {
+      if (l == 0) A.s_out[p] = sv;
+      continue;
+    }
+    if (A.s_out && l == 0) A.s_out[p] = sv;
+    const float yhat = __expf(-A.yeta * sv * sv);
+    float gy;
+    if (!ALIGNED) {
+      gy = yhat - ybar;
+      lossa += 0.5f * gy * gy;
+    } else {
+      const float dl = yhat - label;
+      gy = dl * A.inv_batch;
+      lossa += 0.5f * dl * dl * A.inv_batch;
+    }
+    const float gs = gy * (-2.f * A.yeta * sv * yhat);
+
+    // ================= NTN backward =================
+    const float gmk = (kv & (m > 0.f)) ? (INTENDED ? gs * Uk : gs * usum) : 0.f;
+    if (g == 0) gUa += INTENDED ? gs * rk : gs * rsum;
+    // deferred NTN gradients: this pair's (x1 | 1, x2 | 1, gm)
+    {
+      float *nb_ = A.ntn + (size_t)(uint32_t)p * NBUF;
+      nb_[l] = ((l & (NC - 1)) == D) ? 1.f : sX[l];
+      if (g == 0) nb_[2 * NC + j] = gmk;
+    }
+    const float gmk4 = gmk * A.ik4;
+    float ge[2][8];   // dL/dx · ik4 (before the x > 0 mask) of the lane's rows
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      ge[0][rr] = ge[1][rr] = 0.f;
+      if (rr < KB0) {
+        const int a = 4 * rr + g;
+        const int ac = a < D ? a : 0;
+        ge[0][rr] = row_sum16(gmk4 * (sV[kc * VS + ac] + u[rr]));
+      }
+    }
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      if (rr < KB1) {
+        const int b = 4 * rr + g;
+        const int bc = b < D ? b : 0;
+        ge[1][rr] = row_sum16(gmk4 * (sV[kc * VS + D + bc] + cs[rr]));
+      }
+    }
+
+    // ================= GCN backward, per side =================
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int KB = s ? KB1 : KB0, T = s ? T1 : T0;
+      float af[2][8];
+      load_af(s, T, KB, af);
+      f4 gh2[2];
+#pragma unroll
+      for (int to = 0; to < 2; ++to) {
+        gh2[to] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nb = 4 * to + r;
+          if (nb < KB) {
+            const float gp = xo[s][nb] > 0.f ? ge[s][nb] : 0.f;
+            gwda = fmaf(d2[s][nb], gp, gwda);
+            gbda += gp;
+            const float v = ((kb2[s] >> nb) & 1u) ? gp * wdv * A.ik2 : 0.f;
+            gb1a += v;
+            gh2[to][r] = v;
+          }
+        }
+      }
+      // gZ1 = Âᵀ gH2 (Â symmetric) in both orientations
+      f4 gz1[2], gz1t[2];
+#pragma unroll
+      for (int to = 0; to < 2; ++to) {
+        gz1[to] = gz1t[to] = f4{0.f, 0.f, 0.f, 0.f};
+        if (to < T) {
+#pragma unroll
+          for (int b = 0; b < 8; ++b) {
+            if (b < KB) {
+              gz1[to] = mfma4(af[to][b], gh2[b >> 2][b & 3], gz1[to]);
+              gz1t[to] = mfma4(gh2[b >> 2][b & 3], af[to][b], gz1t[to]);
+            }
+          }
+        }
+      }
+      // gW1 += D1ᵀ gZ1 (D1's C-layout entries are the A operand)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        if (b < KB) {
+#pragma unroll
+          for (int f = 0; f < 2; ++f) gw1[f] = mfma4(d1[s][b >> 2][f][b & 3], gz1[b >> 2][b & 3], gw1[f]);
+        }
+      }
+      // gD1 · ik1 = gZ1 (W1 ik1)ᵀ; gP1 = keep·relu' (D1 > 0); gZ0 = Âᵀ gP1
+      f4 gp1[2][2];   // [to][f]
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        const f4 wt = *(const f4 *)(w1tp + 16 * f * W1S);
+#pragma unroll
+        for (int to = 0; to < 2; ++to) {
+          gp1[to][f] = f4{0.f, 0.f, 0.f, 0.f};
+          if (to < T) {
+            f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) acc = mfma4(gz1t[to][qq], wt[qq], acc);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) gp1[to][f][r] = d1[s][to][f][r] > 0.f ? acc[r] : 0.f;
+            const float gsum = (gp1[to][f][0] + gp1[to][f][1]) + (gp1[to][f][2] + gp1[to][f][3]);
+            if (f) gb0a1 += gsum;
+            else gb0a0 += gsum;
+          }
+        }
+      }
+#pragma unroll
+      for (int to = 0; to < 2; ++to) {
+        if (to < T) {
+          // one-hot Xᵀ rows: type 16τ + j, k-slots 8g + e ↔ node rows 4g + (e & 3)
+          uint4 ohA[2], ohL[2];
+#pragma unroll
+          for (int tau = 0; tau < 2; ++tau) {
+            uint32_t o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              o[r] = (((tyA[s][to] >> (6 * r)) & 63u) == (uint32_t)(16 * tau + j)) ? 0x3F80u : 0u;
+            const uint32_t o01 = o[0] | (o[1] << 16), o23 = o[2] | (o[3] << 16);
+            ohA[tau] = uint4{o01, o23, o01, o23};
+            ohL[tau] = uint4{o01, o23, 0u, 0u};
+          }
+#pragma unroll
+          for (int f = 0; f < 2; ++f) {
+            f4 gz0 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+              if (b < KB) gz0 = mfma4(af[to][b], gp1[b >> 2][f][b & 3], gz0);
+            uint32_t h01, m01, l01, h23, m23, l23;
+            split3(gz0[0], gz0[1], h01, m01, l01);
+            split3(gz0[2], gz0[3], h23, m23, l23);
+            const uint4 bhm = {h01, h23, m01, m23}, bl = {l01, l23, 0u, 0u};
+#pragma unroll
+            for (int tau = 0; tau < 2; ++tau) {
+              gw0[tau][f] = mfbf(ohL[tau], bl, gw0[tau][f]);
+              gw0[tau][f] = mfbf(ohA[tau], bhm, gw0[tau][f]);
+            }
+          }
+        }
+      }
+    }
+  }
+
+  if (!BWD) return;
+  // ---- flush: every wave dumps its slots to LDS, all threads sum the waves ----
+  gb0a0 = xsum32(xsum16(gb0a0));
+  gb0a1 = xsum32(xsum16(gb0a1));
+  gb1a = xsum32(xsum16(gb1a));
+  gwda = xsum32(xsum16(gwda));
+  gbda = xsum32(xsum16(gbda));
+  float *F = smem;
+  __syncthreads();
+  {
+    float *Fw = F + (size_t)wv * NS32 * 64 + l;
+    int s = 0;
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Fw[64 * s++] = gw1[f][r];
+#pragma unroll
+    for (int tau = 0; tau < 2; ++tau)
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Fw[64 * s++] = gw0[tau][f][r] * A.ik0;
+    Fw[64 * s++] = gUa;
+    Fw[64 * s++] = lossa;
+    Fw[64 * s++] = gb0a0;
+    Fw[64 * s++] = gb0a1;
+    Fw[64 * s++] = gb1a;
+    Fw[64 * s++] = gwda;
+    Fw[64 * s++] = gbda;
+  }
+  __syncthreads();
+  float *dst = A.slab + (size_t)blockIdx.x * (size_t)(A.n_params + 1);
+  for (int idx = tid; idx < NS32 * 64; idx += blockDim.x) {
+    const int prm_i = f32_param(A, idx >> 6, idx & 63);
+    if (prm_i < 0) continue;
+    float acc = 0.f;
+    for (int w = 0; w < nw; ++w) acc += F[(size_t)w * NS32 * 64 + idx];
+    dst[prm_i] = acc;
+  }
+}
+
+// ---- NTN gradients: O[a][b'][k] = Σ_p gm_p[k] x1_p[a] x2_p[b'], a, b' <= D ----
+// with x1_p[D] = x2_p[D] = 1: gW = O[a < D][b' < D], gV[k][a] = O[a][D],
+// gV[k][D + b'] = O[D][b'], gb = O[D][D].  Workgroup b sums its contiguous share
+// of the pairs with MFMA: output rows a (two 16-row tiles), columns c = b'·K + k
+// (20 tiles of 16, 4 waves × 5), the pairs are the K dimension (4 per k-step),
+// operands from an LDS-staged chunk.  The result goes to the NTN columns of slab
+// row b (the fused kernel writes the other columns of the same row).
+constexpr int WG_CHUNK = 64;   // pairs staged per LDS round
+
+__global__ void __launch_bounds__(256) sg_ntn_wgrad_kernel(const float *__restrict__ ntn,
+                                                          int64_t n_pairs, int D, int oW,
+                                                          int oV, int obn, int C,
+                                                          float *__restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) float st[WG_CHUNK * NBUF];
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int g = l >> 4, j = l & 15;
+  const int nb = gridDim.x;
+  const int64_t p0 = n_pairs * blockIdx.x / nb, p1 = n_pairs * (blockIdx.x + 1) / nb;
+  const int DK = (D + 1) * FK;   // columns b' <= D
+  // this lane's columns in its wave's 5 column tiles
+  int cb_[5], ck_[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) {
+    const int c = 16 * (w + 4 * t) + j;
+    const int cc = c < DK ? c : 0;
+    cb_[t] = NC + cc / FK;          // x2[b'] offset in the pair's buffer row
+    ck_[t] = c < DK ? 2 * NC + cc % FK : 2 * NC + 15;   // gm[k] (slot 15 is 0: k < FK only)
+  }
+  f4 acc[2][5];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int t = 0; t < 5; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t c0 = p0; c0 < p1; c0 += WG_CHUNK) {
+    const int np = (int)((p1 - c0) < WG_CHUNK ? (p1 - c0) : WG_CHUNK);
+    __syncthreads();
+    for (int i = tid; i < WG_CHUNK * NBUF / 4; i += 256) {
+      const int pp = i / (NBUF / 4);
+      ((f4 *)st)[i] = pp < np ? ((const f4 *)(ntn + (size_t)c0 * NBUF))[i] : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();
+    for (int k0 = 0; k0 < np; k0 += 4) {
+      const float *row = st + (k0 + g) * NBUF;   // pair k0 + g (zero rows past np)
+      const float a0 = row[j], a1 = row[16 + j];
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        const float bv = row[ck_[t]] * row[cb_[t]];
+        acc[0][t] = mfma4(a0, bv, acc[0][t]);
+        acc[1][t] = mfma4(a1, bv, acc[1][t]);
+      }
+    }
+  }
+  float *dst = slab + (size_t)blockIdx.x * C;
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      const int c = 16 * (w + 4 * t) + j;
+      const int bb = c / FK, k = c - bb * FK;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int a = 16 * rt + 4 * g + r;
+        if (a > D || c >= DK) continue;
+        int prm_i;
+        if (a < D) prm_i = bb < D ? oW + (a * D + bb) * FK + k : oV + k * 2 * D + a;
+        else prm_i = bb < D ? oV + k * 2 * D + D + bb : obn + k;
+        dst[prm_i] = acc[rt][t][r];
+      }
+    }
+}
+
+struct F32Cfg {
+  int waves, blocks, shared_floats, wave_floats;
+  size_t lds;
+};
+
+F32Cfg f32_cfg(const SgGenPlan &P, int64_t n_pairs, bool bwd) {
+  F32Cfg c;
+  c.shared_floats = Lds32::shared_floats(P.d_in, P.D);
+  c.wave_floats = Lds32::WAVE;
+  c.waves = MAXW;
+  size_t lds = (size_t)(c.shared_floats + MAXW * c.wave_floats) * 4u;
+  const size_t stage = (size_t)(c.shared_floats + P.n_params) * 4u;
+  const size_t fl = bwd ? (size_t)MAXW * NS32 * 64u * 4u : 0u;
+  if (stage > lds) lds = stage;
+  if (fl > lds) lds = fl;
+  c.lds = lds;
+  const int64_t want = (n_pairs + MAXW - 1) / MAXW;
+  const int64_t cap = (int64_t)sg_num_cus();
+  c.blocks = (int)(want < cap ? (want > 0 ? want : 1) : cap);
+  return c;
+}
+
+}  // namespace
+
+// --------------------------------------------------------------------------
+int sg_fast32_supported(const sg_model_t *m, const SgGenPlan &P) {
+  if (getenv("SG_DISABLE_FAST")) return 0;
+  if (m->num_layers != 5) return 0;
+  const sg_layer_t *Ly = m->layers;
+  if (Ly[0].kind != SG_GCN || !Ly[0].sparse_inputs || Ly[0].output_dim != FH1 ||
+      Ly[0].act != SG_ACT_RELU || !Ly[0].bias)
+    return 0;
+  if (Ly[1].kind != SG_GCN || Ly[1].input_dim != FH1 || Ly[1].output_dim != FH2 ||
+      Ly[1].act != SG_ACT_IDENTITY || !Ly[1].bias)
+    return 0;
+  if (Ly[2].kind != SG_DENSE || Ly[2].input_dim != FH2 || Ly[2].output_dim != 1 ||
+      Ly[2].act != SG_ACT_RELU || !Ly[2].bias)
+    return 0;
+  if (Ly[3].kind != SG_PADDING || Ly[3].padding_value != 0.f) return 0;
+  const int D = Ly[3].output_dim;
+  if (Ly[4].kind != SG_NTN || Ly[4].input_dim != D || Ly[4].output_dim != FK ||
+      Ly[4].act != SG_ACT_RELU || !Ly[4].bias)
+    return 0;
+  if (m->n_max != NC || D <= 12 || D >= NC) return 0;   // slot D of x holds the 1
+  if (m->final_act != SG_FINAL_GAUSSIAN) return 0;
+  if (m->d_in > 32 || m->d_in < 1) return 0;
+  // LDS: the shared tables, 8 wave regions and the flush must fit one CU
+  const size_t lds = (size_t)(Lds32::shared_floats(m->d_in, D) + MAXW * Lds32::WAVE) * 4u;
+  if (lds > 163840u) return 0;
+  return P.n_params > 0 ? 1 : 0;
+}
+
+int64_t sg_fast32_slab_floats(const SgGenPlan &P, int64_t n_pairs) {
+  const F32Cfg c = f32_cfg(P, n_pairs, true);
+  return (int64_t)c.blocks * (P.n_params + 1);
+}
+
+int64_t sg_fast32_ntn_floats(int64_t n_pairs) { return n_pairs * NBUF; }
+
+int sg_fast32_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
+                  const int32_t *order, int64_t n_pairs, int64_t pair_offset,
+                  int64_t batch_total, const float *params, uint64_t seed, const float *y_stats,
+                  float *s_out, float *slab, float *ntn, int *blocks_out, hipStream_t stream) {
+  const F32Cfg c = f32_cfg(P, n_pairs, bwd);
+  if (n_pairs > 0x7FFFFFFF - (int64_t)c.blocks * c.waves * 2) return SG_ERR_ARG;
+  F32Args A;
+  A.recs = (const uint8_t *)recs;
+  A.order = order;
+  A.n_pairs = n_pairs;
+  A.pair_offset = pair_offset;
+  A.rw4h = P.hbm_words / 4;
+  A.rec_bf16 = P.adj_dtype == SG_DTYPE_BF16 ? 1 : 0;
+  A.params = params;
+  A.y_stats = y_stats;
+  A.s_out = s_out;
+  A.slab = slab;
+  A.ntn = ntn;
+  A.key = sg_seed_key(seed);
+  const float keep = m->keep_prob;
+  const float k0 = m->layers[0].dropout ? keep : 1.f, k1 = m->layers[1].dropout ? keep : 1.f;
+  const float k2 = m->layers[2].dropout ? keep : 1.f, k4 = m->layers[4].dropout ? keep : 1.f;
+  A.thr0 = sg_keep_threshold(k0);
+  A.thr1 = sg_keep_threshold(k1);
+  A.thr2 = sg_keep_threshold(k2);
+  A.thr4 = sg_keep_threshold(k4);
+  A.ik0 = 1.f / k0;
+  A.ik1 = 1.f / k1;
+  A.ik2 = 1.f / k2;
+  A.ik4 = 1.f / k4;
+  A.yeta = m->yeta;
+  A.inv_batch = batch_total > 0 ? 1.f / (float)batch_total : 0.f;
+  A.d_in = P.d_in;
+  A.n_params = P.n_params;
+  A.D = P.D;
+  A.shared_floats = c.shared_floats;
+  A.wave_floats = c.wave_floats;
+  A.oW0 = P.L[0].offW;
+  A.ob0 = P.L[0].offB;
+  A.oW1 = P.L[1].offW;
+  A.ob1 = P.L[1].offB;
+  A.oWd = P.L[2].offW;
+  A.obd = P.L[2].offB;
+  A.oW = P.offW;
+  A.oV = P.offV;
+  A.oU = P.offU;
+  A.obn = P.offB;
+  const bool aligned = m->loss_mode == SG_LOSS_ALIGNED;
+  const bool intended = m->ntn_mode == SG_NTN_INTENDED;
+  auto launch = [&](const void *fn, auto kern) {
+    if (c.lds > 65536u)
+      (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds);
+    hipLaunchKernelGGL(kern, dim3(c.blocks), dim3(64 * c.waves), c.lds, stream, A);
+  };
+#define SG32_LAUNCH(B, AL, IN) \
+  launch((const void *)sg_fast32_kernel<B, AL, IN>, sg_fast32_kernel<B, AL, IN>)
+  if (!bwd) {
+    if (intended) SG32_LAUNCH(false, false, true);
+    else SG32_LAUNCH(false, false, false);
+  } else if (aligned) {
+    if (intended) SG32_LAUNCH(true, true, true);
+    else SG32_LAUNCH(true, true, false);
+  } else {
+    if (intended) SG32_LAUNCH(true, false, true);
+    else SG32_LAUNCH(true, false, false);
+  }
+#undef SG32_LAUNCH
+  if (bwd) {
+    hipLaunchKernelGGL(sg_ntn_wgrad_kernel, dim3(c.blocks), dim3(256), 0, stream,
+                       (const float *)ntn, n_pairs, P.D, P.offW, P.offV, P.offB, P.n_params + 1,
+                       slab);
+  }
+  if (blocks_out) *blocks_out = c.blocks;
+  return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
+}

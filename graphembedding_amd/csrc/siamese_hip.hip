@@ -36,6 +36,14 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
                 const int32_t *order, int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
                 uint64_t seed, const float *y_stats, float *s_out, float *slab, int *blocks_out,
                 hipStream_t stream);
+// fused capacity-32 path (sg_fast32.hip)
+int sg_fast32_supported(const sg_model_t *m, const SgGenPlan &P);
+int64_t sg_fast32_slab_floats(const SgGenPlan &P, int64_t n_pairs);
+int64_t sg_fast32_ntn_floats(int64_t n_pairs);
+int sg_fast32_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
+                  const int32_t *order, int64_t n_pairs, int64_t pair_offset,
+                  int64_t batch_total, const float *params, uint64_t seed, const float *y_stats,
+                  float *s_out, float *slab, float *ntn, int *blocks_out, hipStream_t stream);
 
 namespace {
 
@@ -209,7 +217,8 @@ __global__ void __launch_bounds__(256) sg_pack_kernel(const float *__restrict__ 
 // ---- processing order: stable counting sort of the records by cost class ----
 // Key of a record = the cost class of its pair in the kernel that will run it:
 // fused path (N0 > 8) + (N1 > 8) (third Â k-step per side, and the shared-tile
-// PACK body when both sides fit 8 nodes); generic path N0 + N1.  Blocks own
+// PACK body when both sides fit 8 nodes); capacity-32 fused path
+// ceil(N0/4) + ceil(N1/4) (node k-blocks); generic path N0 + N1.  Blocks own
 // contiguous chunks; counts are stored key-major so one exclusive scan gives
 // every (key, chunk) its output base; the scatter keeps record order within a
 // key (ballot ranks), so the permutation is deterministic.
@@ -222,6 +231,8 @@ __device__ __forceinline__ int sg_order_key(const uint8_t *__restrict__ recs, in
   int n0 = r[0], n1 = r[1];
   n0 = n0 < 0 ? 0 : (n0 > nmax ? nmax : n0);
   n1 = n1 < 0 ? 0 : (n1 > nmax ? nmax : n1);
+  // fast: 1 = sg_fast (third k-step per side), 2 = sg_fast32 (k-blocks of 4 nodes)
+  if (fast == 2) return ((n0 + 3) >> 2) + ((n1 + 3) >> 2);
   return fast ? (n0 > 8) + (n1 > 8) : n0 + n1;
 }
 
@@ -373,7 +384,8 @@ int launch_reduce(const float *slab, int nblk, int C, float *part, float *grad, 
 
 struct PathChoice {
   int status;
-  bool fast;
+  int path;   // 0 generic, 1 fused (sg_fast), 2 fused capacity 32 (sg_fast32)
+  bool fast;  // path != 0
   SgGenPlan plan;
 };
 
@@ -381,13 +393,36 @@ PathChoice choose_path(const sg_model_t *m, bool bwd) {
   PathChoice c;
   c.status = sg_build_plan(m, &c.plan);
   c.fast = false;
+  c.path = 0;
   if (c.status != SG_OK) return c;
   if (sg_fast_supported(m, c.plan)) {
     c.fast = true;
+    c.path = 1;
+    return c;
+  }
+  if (sg_fast32_supported(m, c.plan)) {
+    c.fast = true;
+    c.path = 2;
     return c;
   }
   if (!sg_generic_lds_ok(c.plan, bwd)) c.status = SG_ERR_UNSUPPORTED;
   return c;
+}
+
+// workspace layout: [slab rows | reduce partials | (sg_fast32) per-pair NTN buffer];
+// the slab is sized for any path (SG_DISABLE_FAST may route a fused-path model to
+// the generic kernel after the workspace was sized)
+int64_t ntn_offset_floats(const PathChoice &c, int64_t n_pairs) {
+  const int64_t C = c.plan.n_params + 1;
+  int64_t slab = sg_generic_slab_floats(c.plan, n_pairs);
+  if (c.path == 1) {
+    const int64_t f = sg_fast_slab_floats(c.plan, n_pairs);
+    if (f > slab) slab = f;
+  } else if (c.path == 2) {
+    const int64_t f = sg_fast32_slab_floats(c.plan, n_pairs);
+    if (f > slab) slab = f;
+  }
+  return (slab + (int64_t)kReduceStrands * C + 63) & ~(int64_t)63;
 }
 
 }  // namespace
@@ -397,7 +432,7 @@ PathChoice choose_path(const sg_model_t *m, bool bwd) {
 // ===========================================================================
 extern "C" {
 
-int32_t sg_version(void) { return 10200; }   /* 1.2.0: pair processing order */
+int32_t sg_version(void) { return 10300; }   /* 1.3.0: fused capacity-32 path */
 
 int64_t sg_record_bytes(int32_t n_max) { return sg_record_bytes_ex(n_max, SG_DTYPE_F32); }
 
@@ -410,7 +445,7 @@ int32_t sg_model_validate(const sg_model_t *model, int64_t *n_params_out, int32_
   PathChoice c = choose_path(model, true);
   if (c.status != SG_OK) return c.status;
   if (n_params_out) *n_params_out = c.plan.n_params;
-  if (path_out) *path_out = c.fast ? 1 : 0;
+  if (path_out) *path_out = c.path;
   return SG_OK;
 }
 
@@ -420,12 +455,8 @@ int64_t sg_workspace_bytes(const sg_model_t *model, int64_t n_pairs) {
   const int64_t C = c.plan.n_params + 1;
   // room for either path (SG_DISABLE_FAST may route a fast-path model to the
   // generic kernel after the workspace was sized)
-  int64_t slab = sg_generic_slab_floats(c.plan, n_pairs);
-  if (c.fast) {
-    const int64_t f = sg_fast_slab_floats(c.plan, n_pairs);
-    if (f > slab) slab = f;
-  }
-  int64_t bytes = (slab + (int64_t)kReduceStrands * C) * 4;
+  int64_t bytes = ntn_offset_floats(c, n_pairs) * 4;
+  if (c.path == 2) bytes += sg_fast32_ntn_floats(n_pairs) * 4;
   bytes = (bytes + 255) & ~(int64_t)255;
   const int64_t label_bytes = (256 + 2) * 8;
   return (bytes > label_bytes ? bytes : label_bytes) + 256;
@@ -501,8 +532,8 @@ int32_t sg_pair_order(const sg_model_t *model, const void *records, int64_t n_pa
   const int nmax = c.plan.n_max;
   const SgRecLayout rl = sg_rec_layout(nmax, c.plan.adj_dtype);
   const int n_off = rl.adj_words + 2 * nmax;
-  const int fast = c.fast ? 1 : 0;
-  const int K = fast ? 3 : 2 * nmax + 1;
+  const int fast = c.path;
+  const int K = fast == 1 ? 3 : (fast == 2 ? 2 * ((nmax + 3) / 4) + 1 : 2 * nmax + 1);
   const int nb = (int)((n_pairs + kOrderChunk - 1) / kOrderChunk);
   hipStream_t st = (hipStream_t)stream;
   int32_t *cnt = (int32_t *)workspace;
@@ -531,9 +562,13 @@ int32_t sg_forward_ex(const sg_model_t *model, const void *records, const int32_
   if (!records || !params || !s_out) return SG_ERR_ARG;
   PathChoice c = choose_path(model, false);
   if (c.status != SG_OK) return c.status;
-  if (c.fast)
+  if (c.path == 1)
     return sg_fast_run(model, c.plan, false, records, order, n_pairs, pair_offset, n_pairs, params,
                        seed, nullptr, s_out, nullptr, nullptr, (hipStream_t)stream);
+  if (c.path == 2)
+    return sg_fast32_run(model, c.plan, false, records, order, n_pairs, pair_offset, n_pairs,
+                         params, seed, nullptr, s_out, nullptr, nullptr, nullptr,
+                         (hipStream_t)stream);
   return sg_generic_run(c.plan, false, records, order, n_pairs, pair_offset, n_pairs, params, seed,
                         nullptr, s_out, nullptr, nullptr, (hipStream_t)stream);
 }
@@ -570,9 +605,13 @@ int32_t sg_fwd_bwd_ex(const sg_model_t *model, const void *records, const int32_
   if (!records) return SG_ERR_ARG;
   int nblk = 0;
   int rc;
-  if (c.fast)
+  if (c.path == 1)
     rc = sg_fast_run(model, c.plan, true, records, order, n_pairs, pair_offset, batch_total,
                      params, seed, y_stats, s_out, slab, &nblk, st);
+  else if (c.path == 2)
+    rc = sg_fast32_run(model, c.plan, true, records, order, n_pairs, pair_offset, batch_total,
+                       params, seed, y_stats, s_out, slab, slab + ntn_offset_floats(c, n_pairs),
+                       &nblk, st);
   else
     rc = sg_generic_run(c.plan, true, records, order, n_pairs, pair_offset, batch_total, params,
                         seed, y_stats, s_out, slab, &nblk, st);

@@ -91,10 +91,24 @@ class SiameseGCNTNMSE(object):
         self.sim_kernel = create_sim_kernel(f.sim_kernel, f.yeta)
         self.final_act_np = create_activation(f.final_act, self.sim_kernel)
         self.record_dtype = getattr(f, 'record_dtype', 'f32') or 'f32'
-        self.sg = _lib.make_model(self.layers, self.input_dim, self.n_max, 1.0 - f.dropout,
-                                  f.final_act, f.sim_kernel, f.yeta, f.loss_mode, f.ntn_mode,
-                                  self.record_dtype)
+        def make(cap):
+            return _lib.make_model(self.layers, self.input_dim, cap, 1.0 - f.dropout,
+                                   f.final_act, f.sim_kernel, f.yeta, f.loss_mode, f.ntn_mode,
+                                   self.record_dtype)
+        self.sg = make(self.n_max)
         self.n_params, self.kernel_path = _lib.validate(self.sg)
+        # Record node capacity: any capacity >= the largest graph is valid, and the
+        # fused kernels want a specific one (the Padding dim <= 12, or 32 for
+        # Padding dims in (12, 31]: config C4), so take it when the stack qualifies.
+        if self.kernel_path == 0 and pd is not None and self.n_max <= pd:
+            for cap in (pd, 32):
+                if cap <= self.n_max:
+                    continue
+                sg2 = make(cap)
+                n2, path2 = _lib.validate(sg2)
+                if path2:
+                    self.sg, self.n_max, self.n_params, self.kernel_path = sg2, cap, n2, path2
+                    break
         import torch
         self.torch = torch
         init = glorot_flat(self.layers, self.input_dim, f.param_seed) if params is None else \

@@ -139,7 +139,11 @@ int32_t sg_version(void);
  * n_params_out: length of the flat fp32 parameter vector (variables in layer
  * order: GCN weights_0,bias; Dense weights,bias; Attention weights;
  * NTN weights_W[D][D][K], weights_V[K][2D], weights_U[K][1], bias[K]).
- * path_out: 1 = fused MFMA fast path, 0 = generic path.  Host-only, no GPU.
+ * path_out: 1 = fused MFMA path (default stack, n_max = Padding dim <= 12),
+ * 2 = fused capacity-32 MFMA path (default stack, n_max = 32, Padding dim in
+ * (12, 31]: config C4), 0 = generic path.  Host-only, no GPU.
+ * The capacity-32 path needs sg_workspace_bytes(model, n_pairs) of workspace,
+ * which includes 320 B per pair for the NTN weight-gradient operands.
  */
 int32_t sg_model_validate(const sg_model_t *model, int64_t *n_params_out, int32_t *path_out);
 

@@ -66,7 +66,9 @@ class Problem:
         import torch
         model = SiameseGCNTNMSE(self.d_in, self.flags, device=device, n_max=self.n_max,
                                 params=self.params)
-        words = self.store().pack_host(self.pairs, self.labels, dtype=model.record_dtype)
+        # records at the model's node capacity (the fused kernels pick their own)
+        words = GraphStore(self.mgs, model.n_max, self.d_in).pack_host(
+            self.pairs, self.labels, dtype=model.record_dtype)
         recs = torch.from_numpy(words.view(np.int32).reshape(-1)).to(device)
         batch = model.batch_from_records(recs, len(self.pairs), self.labels)
         return model, batch

@@ -1,0 +1,92 @@
+"""The fused capacity-32 kernel (csrc/sg_fast32.hip; config C4: AIDS10k-shaped
+graphs, N <= 30, Padding/NTN input_dim 30) through the C-ABI, against the numpy
+oracle and against the generic kernel.  Tolerance 1e-4 (north_star)."""
+import numpy as np
+import pytest
+
+from _fixtures import run_oracle_step, small_problem
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+# name: (n_max = Padding/NTN dim, node-count range, flag overrides)
+CASES = {
+    'c4_default': (30, 1, 30, {}),
+    'c4_nodrop': (30, 5, 30, dict(dropout=0.0)),
+    'c4_intended_aligned': (30, 5, 30, dict(ntn_mode='intended', loss_mode='aligned')),
+    'c4_bf16_records': (30, 5, 30, dict(record_dtype='bf16')),
+    'd16': (16, 2, 16, {}),
+    'd31_full': (31, 25, 31, {}),
+}
+
+
+def _check_grad(g_gpu, g_ref, tol=TOL):
+    scale = max(1.0, float(np.abs(g_ref).max()))
+    err = float(np.abs(g_gpu - g_ref).max())
+    assert err <= tol * scale, 'max |grad err| {} (scale {})'.format(err, scale)
+
+
+@pytest.mark.parametrize('name', list(CASES))
+def test_fast32_matches_oracle(gpu, name):
+    D, lo, hi, ov = CASES[name]
+    prob = small_problem(n_graphs=14, n_pairs=36, seed=41, n_lo=lo, n_hi=hi, n_max=D,
+                         flags_overrides=ov)
+    model, batch = prob.make_gpu_model(device=gpu)
+    assert model.kernel_path == 2 and model.n_max == 32, (model.kernel_path, model.n_max)
+    seed = 777
+    ref = run_oracle_step(prob, seed)
+    s = model.pred_sim_without_act(batch, seed=seed).cpu().numpy()
+    np.testing.assert_allclose(s, ref.s, rtol=TOL, atol=TOL)
+    model.fwd_bwd(batch, seed=seed)
+    _check_grad(model.grad.cpu().numpy(), ref.grad_mse)
+    loss_mse = float(model.loss_buf[0].item())
+    assert abs(loss_mse - ref.loss_mse) <= TOL * max(1.0, abs(ref.loss_mse))
+    model.apply_adam()
+    reg = float(model.reg_buf[0].item())
+    assert abs(loss_mse + reg - ref.loss) <= TOL * max(1.0, abs(ref.loss))
+    np.testing.assert_allclose(model.params.cpu().numpy(), ref.new_params, rtol=0, atol=2e-5)
+
+
+def test_fast32_matches_generic_and_is_reproducible(gpu, monkeypatch):
+    """2,000 pairs: fused capacity-32 kernel == generic LDS kernel (dropout on);
+    bitwise replay; the class order changes only the gradient's summation order."""
+    import torch
+    prob = small_problem(n_graphs=40, n_pairs=2000, seed=23, n_lo=3, n_hi=30, n_max=30)
+    model, batch = prob.make_gpu_model(device=gpu)
+    assert model.kernel_path == 2
+    seed = 5
+    s32 = model.pred_sim_without_act(batch, seed=seed).cpu().numpy()
+    model.fwd_bwd(batch, seed=seed)
+    g32 = model.grad.clone()
+    l32 = float(model.loss_buf[0].item())
+    model.fwd_bwd(batch, seed=seed)
+    assert torch.equal(g32, model.grad), 'fused32 fwd_bwd is not bitwise reproducible'
+    model.balance(batch)
+    assert np.array_equal(model.pred_sim_without_act(batch, seed=seed).cpu().numpy(), s32)
+    model.fwd_bwd(batch, seed=seed)
+    _check_grad(model.grad.cpu().numpy(), g32.cpu().numpy(), tol=1e-5)
+    batch.order = None
+    monkeypatch.setenv('SG_DISABLE_FAST', '1')
+    s_gen = model.pred_sim_without_act(batch, seed=seed).cpu().numpy()
+    model.fwd_bwd(batch, seed=seed)
+    np.testing.assert_allclose(s32, s_gen, rtol=1e-5, atol=1e-5)
+    _check_grad(g32.cpu().numpy(), model.grad.cpu().numpy(), tol=2e-5)
+    assert abs(l32 - float(model.loss_buf[0].item())) <= 1e-5 * max(1.0, abs(l32))
+
+
+def test_fast32_edge_cases(gpu):
+    """Single-node and 30-node graphs in one batch, and an empty batch."""
+    prob = small_problem(n_graphs=12, n_pairs=30, seed=1, n_lo=1, n_hi=30, n_max=30)
+    ns = [g.number_of_nodes() for g in prob.graphs]
+    used = sorted(ns[i] for i in set(prob.pairs.ravel().tolist()))
+    assert used[0] == 1 and used[-1] == 30, used   # a 1-node and a 30-node graph in the batch
+    model, batch = prob.make_gpu_model(device=gpu)
+    assert model.kernel_path == 2
+    ref = run_oracle_step(prob, 3)
+    np.testing.assert_allclose(model.pred_sim_without_act(batch, seed=3).cpu().numpy(), ref.s,
+                               rtol=TOL, atol=TOL)
+    empty = model.batch_from_records(batch.records[:0], 0, batch.labels[:0],
+                                     y_stats=batch.y_stats)
+    model.fwd_bwd(empty, seed=1)
+    assert float(model.grad.abs().max().item()) == 0.0
