@@ -1,5 +1,9 @@
 """bench.py — Siamese fwd+bwd graph-pairs/s on AIDS700nef-shaped all-pairs.
 
+(--dataset syn_aids10knef: config C4, AIDS10knef-shaped all-pairs, 100.4 M pairs per
+step, Padding/NTN 30 on the capacity-32 fused kernel; records resident when a rank's
+shard fits HBM, else packed chunk by chunk inside the step.)
+
 One step = one pass of the hot path over the whole 700² = 490,000-pair
 all-pairs batch: fused forward + broadcast-MSE loss + backward over this rank's
 pair shard, deterministic gradient reduction, RCCL all-reduce of the flat
@@ -37,18 +41,28 @@ def parse():
                    help='pairs for the CPU baseline (0 = auto, -1 = skip)')
     p.add_argument('--order', choices=('class', 'batch'), default='class',
                    help='record processing order: class-balanced (sg_pair_order) or batch order')
+    p.add_argument('--chunk', type=int, default=4_000_000,
+                   help='C4: pairs per packed chunk when a shard does not fit HBM')
+    p.add_argument('--resident-gb', type=float, default=150.0,
+                   help='C4: keep a shard\'s records resident up to this many GB')
     p.add_argument('--json-out', default='')
     p.add_argument('--emulate-world', type=int, default=0,
                    help='diagnostic: time rank 0\'s share of a W-GPU step on one GPU (no collective)')
     return p.parse_args()
 
 
-def cpu_baseline(gs, labels, flags, n_sample):
+def cpu_baseline(gs, labels, flags, n_sample, D=None):
     """Time the oracle's C restatement (oracle/siamese_cpu.c, OpenMP) on a
     bounded sample of the same all-pairs stream, on this host's cores (all of
-    them, and 1 thread as SURVEY §8(d) asks)."""
+    them, and 1 thread as SURVEY §8(d) asks).  The C port's NTN dim is its record
+    capacity, so C4 (D = 30) is timed on capacity-30 records."""
     sys.path.insert(0, os.path.join(ROOT, 'tests'))
     from oracle import cpu_ref
+    if D is not None and D != gs.n_max:
+        from types import SimpleNamespace
+        from graphembedding_amd.packer import GraphStore
+        gs = SimpleNamespace(graphs=gs.graphs, d_in=gs.d_in, n_max=D,
+                             store=GraphStore(gs.mgs, D, gs.d_in))
     out = cpu_ref.time_allpairs_sample(gs, labels, flags, n_sample)
     one = cpu_ref.time_allpairs_sample(gs, labels, flags, 0, target_s=4.0, threads=1)
     out['value_1thread'] = one['value']
@@ -71,22 +85,41 @@ def main():
     device = torch.device('cuda', local)
 
     from graphembedding_amd import _lib
-    from graphembedding_amd.allpairs import AllPairsShard, load_graph_set
+    from graphembedding_amd.allpairs import AllPairsShard, AllPairsStream, load_graph_set
     from graphembedding_amd.config import Flags
     from graphembedding_amd.model_mse import SiameseGCNTNMSE
     from graphembedding_amd.shard import make_allreduce_hook
 
-    flags = Flags(dropout=args.dropout, record_dtype=args.records)
-    gs = load_graph_set(args.dataset, n_max=10)
+    c4 = args.dataset == 'syn_aids10knef'
+    D = 30 if c4 else 10
+    fl = dict(dropout=args.dropout, record_dtype=args.records)
+    if c4:   # AIDS10k: N <= 30 needs Padding / NTN input_dim 30
+        fl.update(layer_3='Padding:max_in_dims=30,padding_value=0',
+                  layer_4='NTN:input_dim=30,feature_map_dim=10,inneract=relu,dropout=True,'
+                          'bias=True')
+    flags = Flags(**fl)
+    gs = load_graph_set(args.dataset, n_max=32 if c4 else 10)
     labels = gs.label_matrix(flags.yeta)
     model = SiameseGCNTNMSE(gs.d_in, flags, device=device, n_max=gs.n_max)
-    if args.emulate_world > 1 and world == 1:
-        shard = AllPairsShard(gs, labels, 0, args.emulate_world, device=device, dtype=args.records)
+    assert model.n_max == gs.n_max
+    ew = args.emulate_world if (args.emulate_world > 1 and world == 1) else 0
+    srank, sworld = (0, ew) if ew else (rank, world)
+    balance = args.order == 'class'
+    streamed = False
+    if c4:
+        from graphembedding_amd.shard import shard_range
+        a, b = shard_range(len(gs.graphs) ** 2, srank, sworld)
+        from graphembedding_amd.packer import record_words
+        streamed = (b - a) * 4 * record_words(gs.n_max, args.records) > args.resident_gb * 1e9
+    if streamed:
+        shard = AllPairsStream(gs, labels, srank, sworld, device=device, chunk=args.chunk,
+                               dtype=args.records, balance=balance)
+        batch = None
     else:
-        shard = AllPairsShard(gs, labels, rank, world, device=device, dtype=args.records)
-    batch = shard.batch(model, balance=(args.order == 'class'))
+        shard = AllPairsShard(gs, labels, srank, sworld, device=device, dtype=args.records)
+        batch = shard.batch(model, balance=balance)
     hook = make_allreduce_hook() if world > 1 else None
-    model.workspace(batch.n_pairs)
+    model.workspace(shard.chunk if streamed else batch.n_pairs)
     stream = torch.cuda.current_stream()
 
     ev = []
@@ -96,7 +129,10 @@ def main():
             e0 = torch.cuda.Event(enable_timing=True)
             e1 = torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-        model.fwd_bwd(batch, add_label_term=(rank == 0))
+        if streamed:
+            shard.fwd_bwd(model, add_label_term=(rank == 0))
+        else:
+            model.fwd_bwd(batch, add_label_term=(rank == 0))
         if timed:
             e1.record(stream)
             ev.append((e0, e1))
@@ -127,12 +163,12 @@ def main():
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     total_pairs = shard.total
     value = total_pairs * args.steps / elapsed
-    if args.emulate_world > 1 and world == 1:
+    if ew:
         value = shard.n * args.steps / elapsed   # diagnostic: one emulated rank's own rate
     loss = float(model.loss_buf[0].item() + model.reg_buf[0].item())
 
     if rank == 0:
-        flops_pair = gs.flops_per_pair()
+        flops_pair = gs.flops_per_pair(D=D)
         bytes_pair = shard.record_bytes
         kern_pairs_s = shard.n / (kern_ms * 1e-3)
         achieved_tf = kern_pairs_s * flops_pair / 1e12
@@ -148,12 +184,13 @@ def main():
         cpu = None
         if world == 1 and args.cpu_sample >= 0:
             try:
-                cpu = cpu_baseline(gs, labels, flags, args.cpu_sample)
+                cpu = cpu_baseline(gs, labels, flags, args.cpu_sample, D=D)
             except Exception as e:  # reported, never fatal for the GPU number
                 cpu = {'value': None, 'unit': 'graph-pairs/s', 'cores': 0, 'kind': 'port',
                        'sample': 'failed: {}'.format(e)}
         out = {
-            'metric': 'graph-pairs/sec (Siamese fwd+bwd), AIDS700 all-pairs',
+            'metric': 'graph-pairs/sec (Siamese fwd+bwd), {} all-pairs'.format(
+                'AIDS10knef' if c4 else 'AIDS700'),
             'value': value,
             'unit': 'graph-pairs/s',
             'n_gpus': world,
@@ -164,13 +201,19 @@ def main():
             'scaling': 'strong',
             'vs_baseline': None,
             'dtype': 'f32',
-            'data': 'synthetic (AIDS700nef-shaped graphs + GED labels, BASELINE.md §3)',
-            'config': {'workload': 'AIDS700nef all-pairs (700 graphs, 490,000 ordered pairs), '
-                                   'default 5-layer Siamese GCN-NTN, dropout {}'.format(args.dropout),
+            'data': 'synthetic ({}-shaped graphs + GED labels, BASELINE.md §3)'.format(
+                'AIDS10knef' if c4 else 'AIDS700nef'),
+            'config': {'workload': ('AIDS10knef all-pairs (10,018 graphs, N <= 30, {:,} ordered '
+                                    'pairs), Padding/NTN 30' if c4 else
+                                    'AIDS700nef all-pairs (700 graphs, {:,} ordered pairs)'
+                                    ).format(total_pairs) +
+                                   ', default 5-layer Siamese GCN-NTN, dropout {}'.format(args.dropout),
                        'global_batch': total_pairs, 'n_max': gs.n_max, 'd_in': gs.d_in,
                        'kernel_path': _lib.PATH_NAMES[model.kernel_path],
                        'records': '{} Â, {} B/pair'.format(args.records, bytes_pair),
                        'order': args.order,
+                       'inputs': ('packed in chunks of {} pairs inside the step'.format(shard.chunk)
+                                  if streamed else 'records resident in HBM'),
                        'parallelism': 'dp{}'.format(world)},
             'roofline': {'bound': 'mfma', 'achieved': achieved_tf, 'peak': FP32_PEAK_TFLOPS,
                          'unit': 'TFLOP/s', 'frac': achieved_tf / FP32_PEAK_TFLOPS,

@@ -16,7 +16,7 @@ import numpy as np
 
 from .data import synthetic_ged_matrix, synthetic_graphs
 from .graphs import ModelGraph, NodeFeatureOneHotEncoder
-from .packer import GraphStore, pack_device, record_words
+from .packer import GraphStore, pack_device, pack_device_into, record_words
 from .shard import shard_range
 
 
@@ -91,3 +91,80 @@ class AllPairsShard(object):
                                      pair_offset=self.start, batch_total=self.total,
                                      y_stats=self.y_stats)
         return model.balance(b) if balance else b
+
+
+class AllPairsStream(object):
+    """This rank's slice of the all-pairs stream, packed and stepped chunk by chunk.
+
+    For shards whose records do not fit HBM at once: AIDS10knef all-pairs (config
+    C4) is 10,018² = 100.4 M pairs, 850 GB of capacity-32 f32 records.  One device
+    buffer holds `chunk` records; for every chunk the pair ids (p // G, p % G) are
+    generated on the device, packed (sg_pack_pairs_ex) and run through fwd_bwd with
+    pair_offset = the chunk's global start, so dropout masks and the broadcast loss
+    are those of the unchunked step.  The chunk gradients and losses are summed in
+    chunk order (deterministic), leaving model.grad / model.loss_buf as one fwd_bwd
+    over the whole shard would (up to fp32 summation order).
+    """
+
+    def __init__(self, gs: GraphSet, labels: np.ndarray, rank: int = 0, world: int = 1,
+                 device='cuda', chunk: int = 4_000_000, dtype: str = 'f32',
+                 n_pairs: Optional[int] = None, balance: bool = True):
+        import torch
+        self.torch = torch
+        G = len(gs.graphs)
+        self.G = G
+        self.total = int(n_pairs if n_pairs is not None else G * G)
+        self.start, self.end = shard_range(self.total, rank, world)
+        self.n = self.end - self.start
+        self.chunk = int(max(1, min(chunk, max(self.n, 1))))
+        self.dtype = dtype
+        self.store = gs.store
+        self.balance = balance
+        self.device = device
+        flat = labels.reshape(-1)[:self.total]
+        # the shard's labels stay on the device (4 B per pair)
+        self.labels = torch.from_numpy(np.ascontiguousarray(flat[self.start:self.end])).to(device)
+        y = flat.astype(np.float64)
+        ybar = y.mean()
+        self.y_stats = torch.tensor([ybar, 0.5 * ((y - ybar) ** 2).sum()], dtype=torch.float32,
+                                    device=device)
+        self.record_bytes = 4 * record_words(gs.n_max, dtype)
+        self.records = torch.empty(self.chunk * record_words(gs.n_max, dtype), dtype=torch.int32,
+                                   device=device)
+        self.status = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def chunks(self):
+        for c0 in range(self.start, self.end, self.chunk):
+            yield c0, min(self.chunk, self.end - c0)
+
+    def _pack(self, model, c0: int, n: int):
+        torch = self.torch
+        p = torch.arange(c0, c0 + n, dtype=torch.int64, device=self.device)
+        pi = torch.stack([p // self.G, p % self.G], dim=1).to(torch.int32).contiguous()
+        lab = self.labels[c0 - self.start:c0 - self.start + n]
+        pack_device_into(self.store, pi, lab, self.records, self.status, dtype=self.dtype)
+        b = model.batch_from_records(self.records, n, lab, pair_offset=c0,
+                                     batch_total=self.total, y_stats=self.y_stats)
+        return model.balance(b) if self.balance else b
+
+    def fwd_bwd(self, model, add_label_term: bool = True):
+        """One fwd+bwd over the shard; leaves the summed gradient / loss_mse in
+        model.grad / model.loss_buf (like model.fwd_bwd on one batch)."""
+        torch = self.torch
+        acc = None
+        model.workspace(self.chunk)
+        for i, (c0, n) in enumerate(self.chunks()):
+            batch = self._pack(model, c0, n)
+            model.fwd_bwd(batch, add_label_term=(add_label_term and i == 0))
+            if acc is None:
+                acc = model.grad_loss.clone()
+            else:
+                acc += model.grad_loss
+        if acc is None:
+            model.grad_loss.zero_()
+        else:
+            model.grad_loss.copy_(acc)
+
+    def check_status(self):
+        if int(self.status.item()) != 0:
+            raise RuntimeError('sg_pack_pairs reported invalid graph ids')

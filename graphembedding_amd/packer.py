@@ -123,6 +123,20 @@ def pack_device(store: GraphStore, pair_idx, labels=None, device='cuda', stream=
     return recs, status
 
 
+def pack_device_into(store: GraphStore, pair_idx, labels, records, status, stream=None,
+                     dtype: str = 'f32'):
+    """sg_pack_pairs_ex into caller-owned device buffers (no allocation): pair_idx
+    int32 [n,2] and labels float32 [n] (or None) as device tensors, records with
+    room for n records."""
+    from . import _lib
+    adj, types, n = store.to_device(records.device)
+    P = int(pair_idx.shape[0])
+    assert records.numel() >= P * record_words(store.n_max, dtype)
+    if P:
+        _lib.pack_pairs(adj, types, n, store.n_max, pair_idx, labels, records, status,
+                        stream=stream, dtype=dtype)
+
+
 def unpack_host(words: np.ndarray, n_max: int, dtype: str = 'f32'):
     """Split host record words into fields (for tests / debugging); a bf16 Â is
     returned widened to f32."""
