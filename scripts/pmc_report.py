@@ -1,5 +1,5 @@
-"""Summarise rocprofv3 PMC passes of the fused bwd kernel (sg_fast_kernel<.., true, ..>).
-usage: python scripts/pmc_report.py gpurun_out/TAG [n_pairs]"""
+"""Summarise rocprofv3 PMC passes of a fused bwd kernel (sg_fast_kernel<.., true, ..>).
+usage: python scripts/pmc_report.py gpurun_out/TAG [n_pairs] [kernel name, default sg_fast_kernel]"""
 import collections
 import csv
 import glob
@@ -7,11 +7,12 @@ import sys
 
 d = sys.argv[1]
 P = float(sys.argv[2]) if len(sys.argv) > 2 else 490000.0
+KN = sys.argv[3] if len(sys.argv) > 3 else 'sg_fast_kernel'
 acc = collections.defaultdict(list)
 for f in glob.glob(d + '/pass*/run_counter_collection.csv'):
     for r in csv.DictReader(open(f)):
         k = r['Kernel_Name']
-        if 'sg_fast_kernel' in k and 'true' in k.split(',')[1]:
+        if KN + '<' in k and 'true' in k.split('<')[1].split(',')[0 if KN == 'sg_fast32_kernel' else 1]:
             acc[r['Counter_Name']].append(float(r['Counter_Value']))
 m = {k: sum(v) / len(v) for k, v in acc.items()}
 g = m.get('GRBM_GUI_ACTIVE', 0) / 8.0   # per-XCD cycles of the dispatch

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Collect PMC counters for the fused kernel, one rocprofv3 pass per counter group
 # (counters only, no tracing domains).  Usage: scripts/profile_counters.sh OUTDIR [groups...]
+# BENCH_ARGS: extra bench.py arguments (e.g. "--dataset syn_aids10knef --emulate-world 8").
 set -u
 OUT=${1:-gpurun_out/pmc}
 shift || true
@@ -21,7 +22,7 @@ i=0
 for grp in "${GROUPS_LIST[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp -d "$ROOT/$OUT/pass$i" -o run --output-format csv -- \
-    python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample -1 > "$ROOT/$OUT/pass$i.log" 2>&1
+    python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-sample -1 ${BENCH_ARGS:-} > "$ROOT/$OUT/pass$i.log" 2>&1
   rc=$?
   echo "pass $i [$grp] rc=$rc" >> "$ROOT/$OUT/summary.txt"
   if [ $rc -ge 124 ]; then echo "stopping after rc=$rc"; exit $rc; fi
