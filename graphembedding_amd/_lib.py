@@ -91,6 +91,10 @@ def lib():
     L.sg_pair_order_workspace_bytes.restype = c_i64
     L.sg_pair_order.argtypes = [pm, vp, c_i64, vp, vp, vp]
     L.sg_pair_order.restype = c_i32
+    L.sg_sampler_random.argtypes = [vp, vp, c_i32, c_i64, vp, vp]
+    L.sg_sampler_random.restype = c_i32
+    L.sg_sampler_density.argtypes = [vp, vp, vp, c_i32, c_i32, vp, c_i64, vp, vp]
+    L.sg_sampler_density.restype = c_i32
     L.sg_adam_tf.argtypes = [vp, vp, vp, vp, c_i64, c_f, c_f, c_f, c_f, c_f, vp, vp, vp]
     L.sg_adam_tf.restype = c_i32
     _lib = L
@@ -103,7 +107,7 @@ EXPORTED_SYMBOLS = ('sg_version', 'sg_record_bytes', 'sg_record_bytes_ex', 'sg_m
                     'sg_workspace_bytes', 'sg_pack_pairs', 'sg_pack_pairs_ex', 'sg_label_stats',
                     'sg_label_stats_ex', 'sg_forward', 'sg_fwd_bwd', 'sg_adam_tf',
                     'sg_forward_ex', 'sg_fwd_bwd_ex', 'sg_pair_order',
-                    'sg_pair_order_workspace_bytes')
+                    'sg_pair_order_workspace_bytes', 'sg_sampler_random', 'sg_sampler_density')
 
 # sg_dtype: storage type of Â in the pair records
 DTYPES = {'f32': 0, 'bf16': 1}
@@ -254,6 +258,19 @@ def fwd_bwd(m: SgModel, records, n_pairs, pair_offset, batch_total, params, seed
                               int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(y_stats), int(add_label_term),
                               _ptr(s_out), _ptr(grad_out), _ptr(loss_out), _ptr(workspace),
                               _stream(stream)), 'sg_fwd_bwd_ex')
+
+
+def sampler_random(state, sigma, n, count, pairs_out, stream=None):
+    check(lib().sg_sampler_random(_ptr(state), _ptr(sigma), int(n), int(count), _ptr(pairs_out),
+                                  _stream(stream)), 'sg_sampler_random')
+
+
+def sampler_density(state, dens_order, bins, bin_size, item_table, count, pairs_out,
+                    stream=None):
+    check(lib().sg_sampler_density(_ptr(state), _ptr(dens_order), _ptr(bins),
+                                   int(bins.numel()), int(bin_size), _ptr(item_table),
+                                   int(count), _ptr(pairs_out), _stream(stream)),
+          'sg_sampler_density')
 
 
 def adam_tf(params, m, v, grad, lr, beta1, beta2, eps, weight_decay, beta_powers, reg_loss=None,

@@ -1,0 +1,90 @@
+// sg_sampler.hip — device-side pair samplers (model/Siamese/samplers.py:19-68).
+//
+// Every random draw of the reference's samplers comes from a FRESH generator with a
+// known seed: RandomSampler re-shuffles its list with random.Random(123) on every
+// wrap (samplers.py:28), i.e. applies the same permutation σ each time;
+// DistributionSampler walks bins shuffled by random.Random(123) and takes its item
+// index from random.Random(123 + cur).randint(0, bin_size - 1) (samplers.py:51-68).
+// So the host builds σ, the density order, the bin order and the per-cur item table
+// once with CPython's own `random` (graphembedding_amd/device_sampler.py), and these
+// kernels advance the sampler state and emit the pair-id stream on the device, so a
+// training step needs no host work.  Streams equal the reference's bit for bit
+// (tests/test_gpu_sampler.py replays the golden F2 streams).
+#include "sg_plan.h"
+
+namespace {
+
+// state: [0] = idx, [1, 1 + n) = the list (store ids), [1 + n, 1 + 2n) = scratch
+__global__ void __launch_bounds__(1024) sg_sampler_random_kernel(int32_t *__restrict__ st,
+                                                                const int32_t *__restrict__ sigma,
+                                                                int n, int64_t count,
+                                                                int32_t *__restrict__ out) {
+  int32_t *L = st + 1, *tmp = st + 1 + n;
+  const int t = threadIdx.x;
+  int idx = st[0];
+  if (idx < 0 || idx >= n) idx = 0;
+  for (int64_t c = 0; c < count; ++c) {
+    const int g1 = L[idx];
+    ++idx;
+    if (idx >= n) {   // random.Random(123).shuffle(self.gs): L <- L ∘ σ
+      __syncthreads();
+      for (int i = t; i < n; i += blockDim.x) tmp[i] = L[sigma[i]];
+      __syncthreads();
+      for (int i = t; i < n; i += blockDim.x) L[i] = tmp[i];
+      __syncthreads();
+      idx = 0;
+    }
+    if (t == 0) {
+      out[2 * c] = g1;
+      out[2 * c + 1] = L[idx];
+    }
+  }
+  __syncthreads();
+  if (t == 0) st[0] = idx;
+}
+
+// state: [0] = cur, [1] = item_idx
+__global__ void sg_sampler_density_kernel(int32_t *__restrict__ st,
+                                          const int32_t *__restrict__ dens_order,
+                                          const int32_t *__restrict__ bins, int n_bins,
+                                          int bin_size, const int32_t *__restrict__ item_table,
+                                          int64_t count, int32_t *__restrict__ out) {
+  if (threadIdx.x != 0) return;
+  int cur = st[0], item = st[1];
+  for (int64_t c = 0; c < count; ++c) {
+    out[2 * c] = dens_order[bins[cur] * bin_size + item];
+    out[2 * c + 1] = dens_order[bins[cur + 1] * bin_size + item];
+    cur += 2;
+    if (cur >= n_bins - 1) cur = 0;
+    item = item_table[cur >> 1];   // random.Random(123 + cur).randint(0, bin_size - 1)
+  }
+  st[0] = cur;
+  st[1] = item;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t sg_sampler_random(int32_t *state, const int32_t *sigma, int32_t n, int64_t count,
+                          int32_t *pairs_out, sg_stream_t stream) {
+  if (n < 2 || count < 0 || !state || !sigma || (count > 0 && !pairs_out)) return SG_ERR_ARG;
+  if (count == 0) return SG_OK;
+  hipLaunchKernelGGL(sg_sampler_random_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, state,
+                     sigma, n, count, pairs_out);
+  return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
+}
+
+int32_t sg_sampler_density(int32_t *state, const int32_t *dens_order, const int32_t *bins,
+                           int32_t n_bins, int32_t bin_size, const int32_t *item_table,
+                           int64_t count, int32_t *pairs_out, sg_stream_t stream) {
+  if (n_bins < 2 || bin_size < 1 || count < 0 || !state || !dens_order || !bins || !item_table ||
+      (count > 0 && !pairs_out))
+    return SG_ERR_ARG;
+  if (count == 0) return SG_OK;
+  hipLaunchKernelGGL(sg_sampler_density_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, state,
+                     dens_order, bins, n_bins, bin_size, item_table, count, pairs_out);
+  return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
+}
+
+}  // extern "C"

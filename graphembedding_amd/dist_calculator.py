@@ -10,6 +10,8 @@ from __future__ import annotations
 
 from collections import OrderedDict
 
+import numpy as np
+
 from .distance import ged, normalized_dist
 from .utils import get_save_path, safe_load, save
 
@@ -36,7 +38,10 @@ class DistCalculator(object):
         for i, a in enumerate(gids):
             for j, b in enumerate(gids):
                 m[(a, b)] = int(dmat[i][j])
-        return cls(dataset, dist_metric, algo, gidpair_dist_map=m)
+        obj = cls(dataset, dist_metric, algo, gidpair_dist_map=m)
+        # the dense matrix too: device_sampler.label_matrix gathers from it directly
+        obj.matrix = ({g: i for i, g in enumerate(gids)}, np.asarray(dmat))
+        return obj
 
     def calculate_dist(self, g1, g2):
         gid1 = g1.graph['gid']

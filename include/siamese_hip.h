@@ -228,6 +228,25 @@ int32_t sg_fwd_bwd_ex(const sg_model_t *model, const void *records, const int32_
                       void *workspace, sg_stream_t stream);
 
 /*
+ * Device-side pair samplers (library 1.4; samplers.py:19-68).  The reference's
+ * samplers draw only from fresh random.Random(seed) generators with known seeds,
+ * so the host builds their tables once with CPython's `random`; these calls then
+ * advance the sampler state in device memory and write `count` pairs of store
+ * ids to pairs_out [count][2], exactly the reference's get_pair() stream.
+ *   sg_sampler_random (RandomSampler): state [1 + 2n] = idx | current list | scratch,
+ *     sigma [n] = random.Random(123).shuffle(list(range(n))) (applied on each wrap).
+ *   sg_sampler_density (DistributionSampler): state [2] = cur | item_idx,
+ *     dens_order [n] (store ids sorted by (density, idx)), bins [n_bins] (shuffled
+ *     bin ids, truncated to 2 * sample_num), item_table [ceil(n_bins / 2)]:
+ *     entry c / 2 = random.Random(123 + c).randint(0, bin_size - 1).
+ */
+int32_t sg_sampler_random(int32_t *state, const int32_t *sigma, int32_t n, int64_t count,
+                          int32_t *pairs_out, sg_stream_t stream);
+int32_t sg_sampler_density(int32_t *state, const int32_t *dens_order, const int32_t *bins,
+                           int32_t n_bins, int32_t bin_size, const int32_t *item_table,
+                           int64_t count, int32_t *pairs_out, sg_stream_t stream);
+
+/*
  * TF ApplyAdam (training_ops ApplyAdam, non-Nesterov) with the weight-decay
  * gradient wd·θ added first (models.py:69-73):
  *   g = grad + wd·θ; α = lr·√(1-β2^t)/(1-β1^t); m += (g-m)(1-β1);

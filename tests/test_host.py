@@ -129,3 +129,51 @@ def test_feed_dict_sampler_call_pattern():
         batch = model.get_feed_dict(data, None, 'train')
         assert data.calls == expect and batch.n_pairs == 5
         assert batch.records.numel() == 5 * record_words(10)
+
+
+def test_device_sampler_tables_and_state_machine():
+    """Host half of the device samplers (device_sampler.py / csrc/sg_sampler.hip):
+    σ is CPython's shuffle, and the kernel's state machine (idx, L <- L∘σ on
+    wrap), run here in numpy, reproduces RandomSampler.get_pair over many wraps."""
+    import random as pyrandom
+    from graphembedding_amd.device_sampler import shuffle_permutation
+    from graphembedding_amd.samplers import RandomSampler
+    for n in (2, 5, 52, 420):
+        x = list(range(100, 100 + n))
+        y = list(x)
+        pyrandom.Random(123).shuffle(y)
+        sigma = shuffle_permutation(n)
+        assert y == [x[i] for i in sigma]
+        host = RandomSampler(list(range(n)), -1, False)
+        L, idx = np.arange(n), 0
+        for _ in range(3 * n + 7):
+            g1 = L[idx]
+            idx += 1
+            if idx >= n:
+                L, idx = L[sigma], 0
+            assert [g1, L[idx]] == list(host.get_pair())
+        assert list(L) == list(host.gs)
+
+
+def test_label_matrix_matrix_path_equals_lookup_path():
+    """device_sampler.label_matrix: the dense-matrix gather gives the same float32
+    labels as data.get_dist per pair (normalized_dist + Gaussian kernel)."""
+    from graphembedding_amd.config import Flags
+    from graphembedding_amd.data import synthetic_ged_matrix
+    from graphembedding_amd.data_siamese import SiameseModelData
+    from graphembedding_amd.device_sampler import label_matrix
+    from graphembedding_amd.dist_calculator import DistCalculator
+    from graphembedding_amd.similarity import create_sim_kernel
+    f = Flags(dataset='syn_aids80nef')
+    data = SiameseModelData(f)
+    gs = list(data.orig_train_graphs) + [data.test_data.gs[i].nxgraph for i in range(data.m)]
+    dc = DistCalculator.from_matrix(f.dataset, gs, synthetic_ged_matrix(gs))
+
+    class _M:   # the two attributes label_matrix reads
+        flags = f
+        sim_kernel = create_sim_kernel(f.sim_kernel, f.yeta)
+    gl = data.train_data.gs[:20]
+    fast = label_matrix(_M, gl, dc, data)
+    del dc.matrix
+    slow = label_matrix(_M, gl, dc, data)
+    assert fast.dtype == np.float32 and np.array_equal(fast, slow)
