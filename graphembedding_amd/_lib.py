@@ -12,6 +12,8 @@ from typing import List, Optional
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # SG_LIB overrides the in-tree library (A/B builds of kernel variants)
 LIB_PATH = os.environ.get('SG_LIB') or os.path.join(_HERE, 'lib', 'libsiamese_hip.so')
+if not os.path.isabs(LIB_PATH) and not os.path.exists(LIB_PATH):
+    LIB_PATH = os.path.join(os.path.dirname(_HERE), LIB_PATH)   # relative to the repo root
 
 SG_OK, SG_ERR_ARG, SG_ERR_UNSUPPORTED, SG_ERR_HIP, SG_ERR_SHAPE = 0, 1, 2, 3, 4
 _ERR_NAMES = {1: 'SG_ERR_ARG', 2: 'SG_ERR_UNSUPPORTED', 3: 'SG_ERR_HIP', 4: 'SG_ERR_SHAPE'}

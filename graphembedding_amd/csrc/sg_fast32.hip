@@ -36,6 +36,17 @@ constexpr int TS1 = 36;    // D1 transpose tile row stride
 constexpr int W1S = 20;    // W1·ik1 [32][16] row stride
 constexpr int W1TS = 36;   // W1ᵀ [16][32] row stride
 constexpr int WAS = 32;    // Wa[a][k][b] row stride (b)
+constexpr int RS = 34;     // LDS row stride of the record's Â image: 2·ni + g distinct mod 32,
+                           // so an Â fragment read (ds_read_b32) is bank-conflict free
+// Wa rows (row = a·K + k, 128 B; 32 rows of a, zero past D) are read 16 B at a time; a ds_read_b128 lane group
+// holds lanes (a, k) of two row groups, and the identity layout puts ~6 of them on
+// one 16-B bank slot.  The chunk index is XOR-swizzled by f(k, a & 1) (a 3-bit
+// table found by search, scripts/lds_swizzle_search.py) so that every lane group
+// hits distinct slots: conflict-free.  a & 1 = g & 1 for the reading lane.
+constexpr uint32_t WA_SWZ0 = 0x2ccb8ff2u, WA_SWZ1 = 0x17a0853u;
+__device__ __forceinline__ int wa_swz(int k, int a) {
+  return (int)(((a & 1) ? WA_SWZ1 : WA_SWZ0) >> (3 * k)) & 7;
+}
 constexpr int VS = 64;     // V[k][c] row stride (c < 2D)
 constexpr int NBUF = 80;   // NTN buffer floats per pair: x1[32] | x2[32] | gm[16]
 constexpr int MAXW = 8;    // waves per block (2 per SIMD)
@@ -61,15 +72,18 @@ struct F32Args {
   int oW0, ob0, oW1, ob1, oWd, obd, oW, oV, oU, obn;
 };
 
-// per-wave LDS (floats): record image | D1 transpose tile (one side) | x1 | x2 | pad
+// per-wave LDS (floats): record image (Â rows at stride RS, then types, n, label,
+// tag) | D1 transpose tile (one side) | x1 | x2 | pad
 struct Lds32 {
-  static constexpr int RW = 2 * NC * NC + 2 * NC + 4;   // 2116 record words
+  static constexpr int RW = 2 * NC * NC + 2 * NC + 4;   // 2116 HBM record words
+  static constexpr int ADJ = 2 * NC * RS;               // LDS Â image (2176)
+  static constexpr int TAIL = ADJ;                      // types | n | label | tag
   static constexpr int REC = 0;
-  static constexpr int TILE = 2120;
+  static constexpr int TILE = 2248;
   static constexpr int X = TILE + 2 * 16 * TS1;          // x1[32] | x2[32]
   static constexpr int WAVE = X + 72;
   static int shared_floats(int d_in, int D) {
-    return (d_in + 1) * FH1 + D * FK * WAS + FK * VS + FH1 * W1S + FH2 * W1TS;
+    return (d_in + 1) * FH1 + NC * FK * WAS + FK * VS + FH1 * W1S + FH2 * W1TS;
   }
 };
 
@@ -115,7 +129,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
   // ---- parameter staging (behind the shared tables) and tables ----
   float *sW0 = smem;                            // W0 · ik0, row d_in zero
   float *sWa = sW0 + (d_in + 1) * FH1;          // [a][k][WAS]: W[a][b][k] at b
-  float *sV = sWa + D * FK * WAS;               // [k][VS]
+  float *sV = sWa + NC * FK * WAS;              // [k][VS]
   float *sW1 = sV + FK * VS;                    // W1 · ik1 [32][W1S]
   float *sW1T = sW1 + FH1 * W1S;                // W1ᵀ [16][W1TS]
   float *stg = smem + A.shared_floats;
@@ -138,9 +152,10 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
   __syncthreads();
   for (int i = tid; i < (d_in + 1) * FH1; i += blockDim.x)
     sW0[i] = i < d_in * FH1 ? stg[A.oW0 + i] * A.ik0 : 0.f;
-  for (int i = tid; i < D * FK * WAS; i += blockDim.x) {
-    const int a = i / (FK * WAS), rem = i - a * FK * WAS, k = rem / WAS, b = rem - k * WAS;
-    sWa[i] = b < D ? stg[A.oW + (a * D + b) * FK + k] : 0.f;
+  for (int i = tid; i < NC * FK * WAS; i += blockDim.x) {
+    const int row = i / WAS, b = i - row * WAS, a = row / FK, k = row - a * FK;
+    sWa[row * WAS + 4 * ((b >> 2) ^ wa_swz(k, a)) + (b & 3)] =
+        (a < D && b < D) ? stg[A.oW + (a * D + b) * FK + k] : 0.f;
   }
   for (int i = tid; i < FK * VS; i += blockDim.x) {
     const int k = i / VS, c = i - k * VS;
@@ -172,9 +187,11 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
   // per-lane constants: A row of this lane in an Â product = node(to, j) =
   // 16 to + 4 (j % 4) + j / 4, k column 4 b + g (record row stride NC)
   const int ni = 4 * (j & 3) + (j >> 2);
-  const int abase0 = L::REC + ni * NC + g;   // + s·NC² + 16·NC·to + 4 b
+  const int abase0 = L::REC + ni * RS + g;   // + s·NC·RS + 16·RS·to + 4 b
   const float *w1bp = sW1T + j * W1TS + 8 * g;   // W1[8g+q][j] (Z1 = D1 W1)
   const float *w1tp = sW1 + j * W1S + 4 * g;     // ik1·W1[16t+j][4g+q] (gD1)
+  const int wswz = 4 * wa_swz(kc, g);             // Wa chunk swizzle of this lane's rows (floats)
+  const int walane = (g * FK + kc) * WAS;         // + rr·4·FK·WAS (an immediate offset)
 
   // ---- accumulators ----
   f4 gw1[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
@@ -214,32 +231,42 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
         v[c] = w4 < rw4h ? src[w4] : uint4{0u, 0u, 0u, 0u};
       }
       sg_wsync();   // the previous pair's LDS reads are done
+      // HBM word w of the Â block (row r = w / NC, column w % NC) -> LDS r·RS + w % NC
+      auto put4 = [&](int w, f4 v) __attribute__((always_inline)) {
+        float *d = sRec + (w / NC) * RS + (w % NC);
+        *(float2 *)d = float2{v[0], v[1]};
+        *(float2 *)(d + 2) = float2{v[2], v[3]};
+      };
       if (A.rec_bf16) {
 #pragma unroll
         for (int c = 0; c < NREC; ++c) {
           const int w4 = l + 64 * c;
-          if (w4 < ADJ4) {
+          if (w4 < ADJ4) {   // 8 bf16 entries of Â -> 8 f32
             const uint4 x = v[c];
-            f4 lo = {__uint_as_float(x.x << 16), __uint_as_float(x.x & 0xFFFF0000u),
-                     __uint_as_float(x.y << 16), __uint_as_float(x.y & 0xFFFF0000u)};
-            f4 hi = {__uint_as_float(x.z << 16), __uint_as_float(x.z & 0xFFFF0000u),
-                     __uint_as_float(x.w << 16), __uint_as_float(x.w & 0xFFFF0000u)};
-            ((f4 *)sRec)[2 * w4] = lo;
-            ((f4 *)sRec)[2 * w4 + 1] = hi;
+            put4(8 * w4, f4{__uint_as_float(x.x << 16), __uint_as_float(x.x & 0xFFFF0000u),
+                            __uint_as_float(x.y << 16), __uint_as_float(x.y & 0xFFFF0000u)});
+            put4(8 * w4 + 4, f4{__uint_as_float(x.z << 16), __uint_as_float(x.z & 0xFFFF0000u),
+                                __uint_as_float(x.w << 16), __uint_as_float(x.w & 0xFFFF0000u)});
           } else if (w4 < rw4h) {
-            ((uint4 *)sRec)[w4 + ADJ4] = v[c];
+            ((uint4 *)(sRec + L::TAIL))[w4 - ADJ4] = v[c];
           }
         }
       } else {
 #pragma unroll
         for (int c = 0; c < NREC; ++c) {
           const int w4 = l + 64 * c;
-          if (w4 < RW4) ((uint4 *)sRec)[w4] = v[c];
+          if (w4 < 2 * ADJ4) {
+            const uint4 x = v[c];
+            put4(4 * w4, f4{__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z),
+                            __uint_as_float(x.w)});
+          } else if (w4 < RW4) {
+            ((uint4 *)(sRec + L::TAIL))[w4 - 2 * ADJ4] = v[c];
+          }
         }
       }
       sg_wsync();
     }
-    const int *ty = (const int *)sRec + 2 * NC * NC;
+    const int *ty = (const int *)sRec + L::TAIL;
     int N0 = __builtin_amdgcn_readfirstlane(ty[2 * NC]);
     int N1 = __builtin_amdgcn_readfirstlane(ty[2 * NC + 1]);
     N0 = N0 < 0 ? 0 : (N0 > D ? D : N0);
@@ -248,7 +275,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
     const int T0 = N0 > 16 ? 2 : 1, T1 = N1 > 16 ? 2 : 1;
     const int KBm = KB0 > KB1 ? KB0 : KB1;
     const uint32_t pk = sg_pair_key(A.key, (uint32_t)(A.pair_offset + p));
-    const float label = sRec[2 * NC * NC + 2 * NC + 2];
+    const float label = sRec[L::TAIL + 2 * NC + 2];
 
     // ---- layer-0 (node) and NTN-input dropout masks: one hash per lane ----
     // lanes 0..31: layer 0, node e = l; lanes 32..63: layer 4, element e = l - 32
@@ -271,9 +298,9 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
     auto load_af = [&](int s, int T, int KB, float (&af)[2][8]) __attribute__((always_inline)) {
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
-        const int ab = abase0 + s * NC * NC + 4 * b;
+        const int ab = abase0 + s * NC * RS + 4 * b;
         af[0][b] = b < KB ? W[ab] : 0.f;
-        af[1][b] = (b < KB && T > 1) ? W[ab + 16 * NC] : 0.f;
+        af[1][b] = (b < KB && T > 1) ? W[ab + 16 * RS] : 0.f;
       }
     };
 
@@ -300,12 +327,12 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
           tp[b >> 2] |= (k0 ? t_ : 63u) << (6 * (b & 3));
           const float *w0 = sW0 + (k0 ? t_ : (uint32_t)d_in) * FH1 + j;
           const float z0a = w0[0], z0b = w0[16];
-          const int ab = abase0 + s * NC * NC + 4 * b;
+          const int ab = abase0 + s * NC * RS + 4 * b;
           const float a0 = W[ab];
           d1[s][0][0] = mfma4(a0, z0a, d1[s][0][0]);
           d1[s][0][1] = mfma4(a0, z0b, d1[s][0][1]);
           if (T > 1) {
-            const float a1 = W[ab + 16 * NC];
+            const float a1 = W[ab + 16 * RS];
             d1[s][1][0] = mfma4(a1, z0a, d1[s][1][0]);
             d1[s][1][1] = mfma4(a1, z0b, d1[s][1][1]);
           }
@@ -431,12 +458,11 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
       if (bq < KB1) {
         const f4 x2 = *(const f4 *)(sX + NC + 4 * bq);
         float cb[4] = {0.f, 0.f, 0.f, 0.f};
+        const float *wb = sWa + walane + ((4 * bq) ^ wswz);
 #pragma unroll
         for (int rr = 0; rr < 8; ++rr) {
           if (rr < KB0) {
-            const int a = 4 * rr + g;
-            const int ac = a < D ? a : 0;
-            const f4 w = *(const f4 *)(sWa + (ac * FK + kc) * WAS + 4 * bq);
+            const f4 w = *(const f4 *)(wb + rr * 4 * FK * WAS);   // rows a >= D are zero
             const float x1a = xo[0][rr];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {

@@ -29,12 +29,13 @@ if g:
     if 'SQ_LDS_IDX_ACTIVE' in m:
         out['lds_active/cu_cycles'] = m['SQ_LDS_IDX_ACTIVE'] / (g * 256)
         out['lds_bank_conflict/cu_cycles'] = m.get('SQ_LDS_BANK_CONFLICT', 0) / (g * 256)
-for k in ('SQ_INSTS_VALU', 'SQ_INSTS_MFMA', 'SQ_INSTS_LDS'):
+for k in ('SQ_INSTS_VALU', 'SQ_INSTS_MFMA', 'SQ_INSTS_LDS', 'SQ_INSTS_BRANCH', 'SQ_INSTS_SALU',
+          'SQ_INSTS_SMEM', 'SQ_INSTS_VMEM_RD', 'SQ_INSTS_VMEM_WR'):
     if k in m:
         out[k + '/pair'] = m[k] / P
 if 'SQ_WAVE_CYCLES' in m:
     w = m['SQ_WAVE_CYCLES']
-    for k in ('SQ_WAIT_ANY', 'SQ_WAIT_INST_ANY', 'SQ_ACTIVE_INST_ANY'):
+    for k in ('SQ_WAIT_ANY', 'SQ_WAIT_INST_ANY', 'SQ_ACTIVE_INST_ANY', 'SQ_WAIT_INST_LDS'):
         out[k + '/wave_cycles'] = m.get(k, 0) / w
 for k, v in out.items():
     print('{:36s} {:.4g}'.format(k, v))
