@@ -43,6 +43,13 @@ class SgModel(ctypes.Structure):
                 ('layers', SgLayer * SG_MAX_LAYERS), ('adj_dtype', ctypes.c_int32)]
 
 
+class SgCsrStore(ctypes.Structure):
+    """sg_csr_store_t: host struct of device pointers (graph-store path, config C5)."""
+    _fields_ = [('n_graphs', ctypes.c_int32), ('n_max', ctypes.c_int32),
+                ('node_off', ctypes.c_void_p), ('types', ctypes.c_void_p),
+                ('row_ptr', ctypes.c_void_p), ('col', ctypes.c_void_p), ('val', ctypes.c_void_p)]
+
+
 class SiameseHipError(RuntimeError):
     pass
 
@@ -59,6 +66,11 @@ def lib():
         raise SiameseHipError(
             'libsiamese_hip.so not found at {} — run `python -c "import __graft_entry__ as g; '
             'g.build()"` (hipcc --offload-arch=gfx950). There is no CPU fallback.'.format(LIB_PATH))
+    try:   # bring up torch's HIP runtime before the library's first HIP call
+        import torch
+        torch.cuda.is_available()
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     c_i32, c_i64, c_u64, c_f = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float
     vp = ctypes.c_void_p
@@ -99,17 +111,32 @@ def lib():
     L.sg_sampler_density.restype = c_i32
     L.sg_adam_tf.argtypes = [vp, vp, vp, vp, c_i64, c_f, c_f, c_f, c_f, c_f, vp, vp, vp]
     L.sg_adam_tf.restype = c_i32
+    L.sg_adam_workspace_bytes.argtypes = [c_i64]
+    L.sg_adam_workspace_bytes.restype = c_i64
+    L.sg_adam_tf_ex.argtypes = [vp, vp, vp, vp, c_i64, c_f, c_f, c_f, c_f, c_f, vp, vp, vp, vp]
+    L.sg_adam_tf_ex.restype = c_i32
+    pc = ctypes.POINTER(SgCsrStore)
+    L.sg_web_workspace_bytes.argtypes = [pm, c_i64]
+    L.sg_web_workspace_bytes.restype = c_i64
+    L.sg_web_forward.argtypes = [pm, pc, vp, c_i64, c_i64, vp, c_u64, vp, vp, c_i64, vp]
+    L.sg_web_forward.restype = c_i32
+    L.sg_web_fwd_bwd.argtypes = [pm, pc, vp, vp, c_i64, c_i64, c_i64, vp, c_u64, vp, c_i32, vp,
+                                 vp, vp, vp, c_i64, vp]
+    L.sg_web_fwd_bwd.restype = c_i32
     _lib = L
     return L
 
 
-PATH_NAMES = {0: 'generic', 1: 'fused', 2: 'fused32'}
+PATH_NAMES = {0: 'generic', 1: 'fused', 2: 'fused32', 3: 'web'}
+PATH_WEB = 3
 
 EXPORTED_SYMBOLS = ('sg_version', 'sg_record_bytes', 'sg_record_bytes_ex', 'sg_model_validate',
                     'sg_workspace_bytes', 'sg_pack_pairs', 'sg_pack_pairs_ex', 'sg_label_stats',
                     'sg_label_stats_ex', 'sg_forward', 'sg_fwd_bwd', 'sg_adam_tf',
                     'sg_forward_ex', 'sg_fwd_bwd_ex', 'sg_pair_order',
-                    'sg_pair_order_workspace_bytes', 'sg_sampler_random', 'sg_sampler_density')
+                    'sg_pair_order_workspace_bytes', 'sg_sampler_random', 'sg_sampler_density',
+                    'sg_adam_workspace_bytes', 'sg_adam_tf_ex', 'sg_web_workspace_bytes',
+                    'sg_web_forward', 'sg_web_fwd_bwd')
 
 # sg_dtype: storage type of Â in the pair records
 DTYPES = {'f32': 0, 'bf16': 1}
@@ -187,7 +214,8 @@ def make_model(layers: List[dict], d_in: int, n_max: int, keep_prob: float, fina
 
 def validate(m: SgModel):
     """Returns (n_params, path): path 1 = fused kernel (sg_fast), 2 = fused capacity-32
-    kernel (sg_fast32, config C4), 0 = generic kernel."""
+    kernel (sg_fast32, config C4), 3 = graph-store path (sg_web_*, config C5),
+    0 = generic kernel."""
     n = ctypes.c_int64(0)
     p = ctypes.c_int32(0)
     check(lib().sg_model_validate(ctypes.byref(m), ctypes.byref(n), ctypes.byref(p)),
@@ -280,3 +308,49 @@ def adam_tf(params, m, v, grad, lr, beta1, beta2, eps, weight_decay, beta_powers
     check(lib().sg_adam_tf(_ptr(params), _ptr(m), _ptr(v), _ptr(grad), int(params.numel()),
                            float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
                            _ptr(beta_powers), _ptr(reg_loss), _stream(stream)), 'sg_adam_tf')
+
+
+def adam_tf_ex(params, m, v, grad, lr, beta1, beta2, eps, weight_decay, beta_powers, reg_loss,
+               workspace, stream=None):
+    check(lib().sg_adam_tf_ex(_ptr(params), _ptr(m), _ptr(v), _ptr(grad), int(params.numel()),
+                              float(lr), float(beta1), float(beta2), float(eps),
+                              float(weight_decay), _ptr(beta_powers), _ptr(reg_loss),
+                              _ptr(workspace), _stream(stream)), 'sg_adam_tf_ex')
+
+
+def adam_workspace_bytes(n: int) -> int:
+    return int(lib().sg_adam_workspace_bytes(int(n)))
+
+
+def csr_struct(n_graphs, n_max, node_off, types, row_ptr, col, val) -> SgCsrStore:
+    s = SgCsrStore()
+    s.n_graphs = int(n_graphs)
+    s.n_max = int(n_max)
+    s.node_off, s.types, s.row_ptr = _ptr(node_off), _ptr(types), _ptr(row_ptr)
+    s.col, s.val = _ptr(col), _ptr(val)
+    return s
+
+
+def web_workspace_bytes(m: SgModel, chunk: int) -> int:
+    b = int(lib().sg_web_workspace_bytes(ctypes.byref(m), int(chunk)))
+    if b < 0:
+        raise SiameseHipError('sg_web_workspace_bytes: model is not on the graph-store path')
+    return b
+
+
+def web_forward(m: SgModel, store: SgCsrStore, pairs, n_pairs, pair_offset, params, seed, s_out,
+                workspace, chunk, stream=None):
+    check(lib().sg_web_forward(ctypes.byref(m), ctypes.byref(store), _ptr(pairs), int(n_pairs),
+                               int(pair_offset), _ptr(params), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                               _ptr(s_out), _ptr(workspace), int(chunk), _stream(stream)),
+          'sg_web_forward')
+
+
+def web_fwd_bwd(m: SgModel, store: SgCsrStore, pairs, labels, n_pairs, pair_offset, batch_total,
+                params, seed, y_stats, add_label_term, s_out, grad_out, loss_out, workspace, chunk,
+                stream=None):
+    check(lib().sg_web_fwd_bwd(ctypes.byref(m), ctypes.byref(store), _ptr(pairs), _ptr(labels),
+                               int(n_pairs), int(pair_offset), int(batch_total), _ptr(params),
+                               int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(y_stats), int(add_label_term),
+                               _ptr(s_out), _ptr(grad_out), _ptr(loss_out), _ptr(workspace),
+                               int(chunk), _stream(stream)), 'sg_web_fwd_bwd')

@@ -9,7 +9,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(_HERE, 'csrc')
 OUT = os.path.join(_HERE, 'lib', 'libsiamese_hip.so')
 SOURCES = ['siamese_hip.hip', 'sg_generic.hip', 'sg_fast.hip', 'sg_fast32.hip',
-           'sg_sampler.hip']
+           'sg_sampler.hip', 'sg_web.hip']
 HEADERS = ['sg_common.h', 'sg_plan.h', 'sg_mfma.h']
 ARCH = os.environ.get('SG_OFFLOAD_ARCH', 'gfx950')
 

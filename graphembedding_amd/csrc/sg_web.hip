@@ -1,0 +1,1162 @@
+// sg_web.hip — graph-store path for Web-sized graphs (BASELINE config C5; path 3).
+//
+// The reference's default stack (config.py:44-66) with Padding / NTN widened to
+// D in [32, 512] (quirk A9: tf.pad needs N <= max_in_dims):
+//   GCN(d_in→32, relu, sparse one-hot) → GCN(32→16, identity) → Dense(16→1, relu)
+//   → Padding(D) → NTN(D, K ≤ 16) → final act → broadcast / aligned MSE.
+// Dense pair records stop scaling at a few dozen nodes (Â is n_max² per side), so
+// this path reads the graphs from a CSR store and a list of pair ids, and splits
+// a pair's work in two kinds of kernels:
+//
+//  * per graph instance (pair, side): one 8-wave workgroup stages the instance's
+//    activations in LDS (up to 512 nodes) and runs the GCN / Dense / Padding stack
+//    (layers.py:91-118, 192-227).  The sparse products Â·Z run on VALU over the CSR
+//    rows; the dense ones (D1·W1, gZ1·W1ᵀ, D1ᵀ·gZ1 and the one-hot Xᵀ·gZ0) on
+//    v_mfma_f32_16x16x4_f32 with the instance's nodes as 16-row tiles.  Forward
+//    writes the NTN input x (after its dropout) per pair and side; backward
+//    recomputes the forward and accumulates the GCN/Dense gradients per workgroup.
+//  * NTN (layers.py:282-310) as batched GEMMs over the pairs, 128×128 f32 MFMA
+//    tiles: T[p][k][a] = Σ_b W[a][b][k] x2[p][b] (forward), gx2 = (gm ⊗ x1)·W
+//    and gW[k] = Σ_p (gm_k x1)ᵀ x2 (backward).  A per-pair head kernel turns T into
+//    m_k, s, ŷ, the loss and gm = ∂L/∂m, and gx1 = Σ_k gm_k (T_k + V_k).
+//    Tiles whose feature range lies beyond every pair's node count (x is zero
+//    there when padding_value = 0) are skipped: callers that order pairs by size
+//    (web.py) make the tiles homogeneous.
+//
+// Dropout keys, masks and loss conventions are those of the pair-record kernels
+// (sg_common.h; oracle/siamese_oracle.py): pair i of the list is pair_offset + i.
+// Reductions run in a fixed order: results are bitwise reproducible.
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "sg_common.h"
+#include "sg_mfma.h"
+
+int sg_num_cus();
+
+namespace {
+using sgk::f4;
+using sgk::mfma4;
+
+constexpr int WH1 = 32, WH2 = 16;   // GCN widths of the default stack
+constexpr int WKP = 16;             // NTN K capacity (gm rows, head slab)
+constexpr int WMAXD = 512;          // max Padding / NTN width (LDS budget of one instance)
+constexpr int GW = 8;               // waves per instance workgroup
+constexpr int TB = 128;             // GEMM tile edge
+constexpr int MKS = 20;             // MK LDS tile row stride (16 + 4): conflict-free b128 reads
+constexpr int KMS = TB + 4;         // KM LDS tile row stride
+constexpr int HSLAB = 1 + 2 * WKP;  // head slab row: loss | gU[16] | gb[16]
+constexpr int WSPLIT = 8;           // split-K over pairs of the weight-gradient GEMMs
+
+struct WebPlan {
+  int d_in, D, Dp, K;
+  int n_params, n_gcn;
+  int ob0, oW1, ob1, oWd, obd, oW, oV, oU, obn;
+  uint32_t thr0, thr1, thr2, thr4;
+  float ik0, ik1, ik2, ik4;
+  float padv;
+  int final_act, loss_mode, ntn_mode;
+  float yeta;
+  int tb;  // 16-row type tiles of the one-hot gW0 product
+};
+
+int web_plan(const sg_model_t *m, WebPlan *W) {
+  if (!m || !W) return SG_ERR_ARG;
+  memset(W, 0, sizeof(*W));
+  if (m->num_layers != 5) return SG_ERR_UNSUPPORTED;
+  const sg_layer_t *L = m->layers;
+  if (L[0].kind != SG_GCN || !L[0].sparse_inputs || L[0].output_dim != WH1 ||
+      L[0].act != SG_ACT_RELU || !L[0].bias)
+    return SG_ERR_UNSUPPORTED;
+  if (L[0].input_dim > 0 && L[0].input_dim != m->d_in) return SG_ERR_ARG;
+  if (L[1].kind != SG_GCN || L[1].sparse_inputs || L[1].input_dim != WH1 ||
+      L[1].output_dim != WH2 || L[1].act != SG_ACT_IDENTITY || !L[1].bias)
+    return SG_ERR_UNSUPPORTED;
+  if (L[2].kind != SG_DENSE || L[2].input_dim != WH2 || L[2].output_dim != 1 ||
+      L[2].act != SG_ACT_RELU || !L[2].bias)
+    return SG_ERR_UNSUPPORTED;
+  if (L[3].kind != SG_PADDING) return SG_ERR_UNSUPPORTED;
+  const int D = L[3].output_dim;
+  if (D < 32 || D > WMAXD) return SG_ERR_UNSUPPORTED;
+  if (L[4].kind != SG_NTN || L[4].input_dim != D || L[4].output_dim < 1 ||
+      L[4].output_dim > WKP || L[4].act != SG_ACT_RELU)
+    return SG_ERR_UNSUPPORTED;
+  if (m->d_in <= 0 || m->d_in > 64) return SG_ERR_UNSUPPORTED;
+  if (m->n_max <= 0) return SG_ERR_ARG;
+  if (m->n_max > D) return SG_ERR_SHAPE;   // tf.pad with N > max_in_dims (A9)
+  if (!(m->keep_prob > 0.f && m->keep_prob <= 1.f)) return SG_ERR_ARG;
+  if (m->final_act < SG_FINAL_GAUSSIAN || m->final_act > SG_FINAL_TANH) return SG_ERR_ARG;
+  if (m->loss_mode != SG_LOSS_BROADCAST && m->loss_mode != SG_LOSS_ALIGNED) return SG_ERR_ARG;
+  if (m->ntn_mode != SG_NTN_REFERENCE && m->ntn_mode != SG_NTN_INTENDED) return SG_ERR_ARG;
+  W->d_in = m->d_in;
+  W->D = D;
+  W->Dp = (D + TB - 1) / TB * TB;
+  W->K = L[4].output_dim;
+  W->tb = (m->d_in + 15) / 16;
+  int off = m->d_in * WH1;   // W0 at 0
+  W->ob0 = off; off += WH1;
+  W->oW1 = off; off += WH1 * WH2;
+  W->ob1 = off; off += WH2;
+  W->oWd = off; off += WH2;
+  W->obd = off; off += 1;
+  W->n_gcn = off;
+  W->oW = off; off += D * D * W->K;
+  W->oV = off; off += W->K * 2 * D;
+  W->oU = off; off += W->K;
+  W->obn = -1;
+  if (L[4].bias) { W->obn = off; off += W->K; }
+  W->n_params = off;
+  const float keep = m->keep_prob;
+  const float k0 = L[0].dropout ? keep : 1.f, k1 = L[1].dropout ? keep : 1.f;
+  const float k2 = L[2].dropout ? keep : 1.f, k4 = L[4].dropout ? keep : 1.f;
+  W->thr0 = sg_keep_threshold(k0);
+  W->thr1 = sg_keep_threshold(k1);
+  W->thr2 = sg_keep_threshold(k2);
+  W->thr4 = sg_keep_threshold(k4);
+  W->ik0 = 1.f / k0;
+  W->ik1 = 1.f / k1;
+  W->ik2 = 1.f / k2;
+  W->ik4 = 1.f / k4;
+  W->padv = L[3].padding_value;
+  W->final_act = m->final_act;
+  W->loss_mode = m->loss_mode;
+  W->ntn_mode = m->ntn_mode;
+  W->yeta = m->yeta;
+  return SG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Workspace layout (floats unless noted), for chunks of up to `chunk` pairs.
+// ---------------------------------------------------------------------------
+struct WebWs {
+  int64_t Cp;                                        // chunk rounded up to TB
+  int64_t X, GX, T, GM, EXT, EXT16, EXT128;          // per-chunk buffers
+  int64_t Wg, Wh, GWS, GVS, GSLAB, HSLABo, total;    // per-call buffers
+  int gcn_blocks, head_blocks;
+};
+
+int gcn_blocks_for() { return sg_num_cus(); }
+int head_blocks_for() { return 2 * sg_num_cus(); }
+
+WebWs web_ws(const WebPlan &W, int64_t chunk) {
+  WebWs w;
+  if (chunk < 1) chunk = 1;
+  w.Cp = (chunk + TB - 1) / TB * TB;
+  const int64_t Dp = W.Dp, K = W.K;
+  int64_t o = 0;
+  auto take = [&](int64_t n) { const int64_t r = o; o += (n + 63) & ~(int64_t)63; return r; };
+  w.X = take(2 * w.Cp * Dp);        // X1 | X2
+  w.GX = take(2 * w.Cp * Dp);       // gX1 | gX2
+  w.T = take(w.Cp * K * Dp);
+  w.GM = take(w.Cp * WKP);
+  w.EXT = take(2 * w.Cp);           // int2 per pair
+  w.EXT16 = take(2 * (w.Cp / 16));
+  w.EXT128 = take(2 * (w.Cp / TB));
+  w.Wg = take(K * Dp * Dp);
+  w.Wh = take(K * Dp * Dp);
+  w.GWS = take((int64_t)WSPLIT * K * Dp * Dp);
+  w.GVS = take((int64_t)WSPLIT * WKP * 2 * Dp);
+  w.gcn_blocks = gcn_blocks_for();
+  w.head_blocks = head_blocks_for();
+  w.GSLAB = take((int64_t)w.gcn_blocks * W.n_gcn);
+  w.HSLABo = take((int64_t)w.head_blocks * 4 * HSLAB);
+  w.total = o;
+  return w;
+}
+
+// ---------------------------------------------------------------------------
+// Per-pair extents: e = n (padding_value 0: x is zero beyond the graph's nodes)
+// or D; per 16- and 128-pair maxima for the GEMM tile skips.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(TB) web_ext_kernel(const int32_t *__restrict__ pairs, int64_t n,
+                                                     const int32_t *__restrict__ node_off,
+                                                     int full, int D, int2 *__restrict__ ext,
+                                                     int2 *__restrict__ ext16,
+                                                     int2 *__restrict__ ext128) {
+  __shared__ int2 red[2];
+  const int64_t p = (int64_t)blockIdx.x * TB + threadIdx.x;
+  int e1 = 0, e2 = 0;
+  if (p < n) {
+    const int g1 = pairs[2 * p], g2 = pairs[2 * p + 1];
+    e1 = full ? D : node_off[g1 + 1] - node_off[g1];
+    e2 = full ? D : node_off[g2 + 1] - node_off[g2];
+  }
+  ext[p] = make_int2(e1, e2);
+  int m1 = e1, m2 = e2;
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+    m1 = max(m1, __shfl_xor(m1, o, 64));
+    m2 = max(m2, __shfl_xor(m2, o, 64));
+  }
+  if ((threadIdx.x & 15) == 0) ext16[p >> 4] = make_int2(m1, m2);
+#pragma unroll
+  for (int o = 16; o < 64; o <<= 1) {
+    m1 = max(m1, __shfl_xor(m1, o, 64));
+    m2 = max(m2, __shfl_xor(m2, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = make_int2(m1, m2);
+  __syncthreads();
+  if (threadIdx.x == 0)
+    ext128[blockIdx.x] = make_int2(max(red[0].x, red[1].x), max(red[0].y, red[1].y));
+}
+
+// ---------------------------------------------------------------------------
+// Weight layouts for the GEMMs: Wg[k][a][b] = W[a][b][k] (T: rows a, contraction b)
+// and Wh[k][b][a] (gx2: rows b, contraction a); zero beyond D.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) web_wprep_g(const float *__restrict__ Wt, int D, int Dp,
+                                                   int K, float *__restrict__ Wg) {
+  // block: one row a, 64 b's; reads W[a][b0..b0+63][0..K) (contiguous), writes Wg rows
+  __shared__ float t[64 * (WKP + 1)];
+  const int a = blockIdx.x, b0 = blockIdx.y * 64;
+  const int span = 64 * K;
+  for (int i = threadIdx.x; i < span; i += 256) {
+    const int b = b0 + i / K, k = i % K;
+    t[(i / K) * (WKP + 1) + k] = (a < D && b < D) ? Wt[((size_t)a * D + b) * K + k] : 0.f;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < span; i += 256) {
+    const int k = i >> 6, bl = i & 63;
+    Wg[((size_t)k * Dp + a) * Dp + b0 + bl] = t[bl * (WKP + 1) + k];
+  }
+}
+
+__global__ void __launch_bounds__(256) web_wprep_h(const float *__restrict__ Wg, int Dp,
+                                                   float *__restrict__ Wh) {
+  // 32×32 tiled transpose of each Wg[k]
+  __shared__ float t[32][33];
+  const int k = blockIdx.z, x0 = blockIdx.x * 32, y0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const float *src = Wg + (size_t)k * Dp * Dp;
+  float *dst = Wh + (size_t)k * Dp * Dp;
+  for (int r = ty; r < 32; r += 8) t[r][tx] = src[(size_t)(y0 + r) * Dp + x0 + tx];
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8) dst[(size_t)(x0 + r) * Dp + y0 + tx] = t[tx][r];
+}
+
+// ---------------------------------------------------------------------------
+// Per-instance GCN → Dense → Padding stack (+ backward with recompute).
+// ---------------------------------------------------------------------------
+struct GcnArgs {
+  const int32_t *node_off, *types, *row_ptr, *col;
+  const float *val;
+  const int32_t *pairs;
+  int64_t n_pairs, pair_offset, Cp;
+  const float *params;
+  float *X;          // [2][Cp][Dp] NTN inputs (forward)
+  const float *GX;   // [2][Cp][Dp] ∂L/∂x (backward)
+  float *slab;       // [gridDim.x][n_gcn] (backward, accumulated)
+  uint32_t key, thr0, thr1, thr2, thr4;
+  float ik0, ik1, ik2, ik4, padv;
+  int d_in, D, Dp, n_gcn, n_max;
+  int ob0, oW1, ob1, oWd, obd;
+};
+
+// LDS (floats): tables, then the instance region sized for n_max nodes
+//   sW0 [(d_in+1)][32] = W0·ik0 (row d_in zero: dropped one-hot rows), sb0 [32],
+//   sW1 [32][16] = W1·ik1, sW1T [16][32] = (W1·ik1)ᵀ, sb1 [16], sWd [16] = Wd·ik2
+//   sEt [N16] effective type (d_in when dropped / absent), sZ1 [N16][16],
+//   sD1 [N16][32] (backward: D1' = H1·m1, later gP0), sG1 [N16][16] (backward: gZ1)
+struct GcnLds {
+  int w0, b0, w1, w1t, b1, wd, tables, et, z1, d1, g1, total;
+};
+
+__host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, bool bwd) {
+  GcnLds L;
+  int o = 0;
+  L.w0 = o; o += (d_in + 1) * WH1;
+  L.b0 = o; o += WH1;
+  L.w1 = o; o += WH1 * WH2;
+  L.w1t = o; o += WH1 * WH2;
+  L.b1 = o; o += WH2;
+  L.wd = o; o += WH2;
+  o = (o + 3) & ~3;
+  L.tables = o;
+  L.et = o; o += n16;
+  L.z1 = o; o += n16 * WH2;
+  L.d1 = o; if (bwd) o += n16 * WH1;
+  L.g1 = o; if (bwd) o += n16 * WH2;
+  L.total = o;
+  return L;
+}
+
+template <bool BWD, int NTB>
+__global__ void __launch_bounds__(64 * GW) web_gcn_kernel(GcnArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int i = l & 15, g = l >> 4;
+  const int d_in = A.d_in;
+  const int n16max = (A.n_max + 15) & ~15;
+  const GcnLds L = gcn_lds(d_in, n16max, BWD);
+  float *sW0 = sm + L.w0, *sb0 = sm + L.b0, *sW1 = sm + L.w1, *sW1T = sm + L.w1t;
+  float *sb1 = sm + L.b1, *sWd = sm + L.wd;
+  int *sEt = (int *)(sm + L.et);
+  float *sZ1 = sm + L.z1, *sD1 = sm + L.d1, *sG1 = sm + L.g1;
+  const float *prm = A.params;
+  for (int x = tid; x < (d_in + 1) * WH1; x += 64 * GW)
+    sW0[x] = x < d_in * WH1 ? prm[x] * A.ik0 : 0.f;
+  for (int x = tid; x < WH1 * WH2; x += 64 * GW) {
+    const float v = prm[A.oW1 + x] * A.ik1;
+    sW1[x] = v;
+    sW1T[(x % WH2) * WH1 + x / WH2] = v;
+  }
+  if (tid < WH1) sb0[tid] = prm[A.ob0 + tid];
+  if (tid < WH2) {
+    sb1[tid] = prm[A.ob1 + tid];
+    sWd[tid] = prm[A.oWd + tid] * A.ik2;
+  }
+  const float bd = prm[A.obd];
+
+  // gradient accumulators (backward), persistent over the block's instances
+  f4 aW0[NTB][2], aW1[2];
+  float aB0[2] = {0.f, 0.f}, aB1[4] = {0.f, 0.f, 0.f, 0.f}, aWd[4] = {0.f, 0.f, 0.f, 0.f};
+  float aBd = 0.f;
+#pragma unroll
+  for (int t = 0; t < NTB; ++t) aW0[t][0] = aW0[t][1] = f4{0.f, 0.f, 0.f, 0.f};
+  aW1[0] = aW1[1] = f4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+
+  const int64_t n_inst = 2 * A.n_pairs;
+  for (int64_t q = blockIdx.x; q < n_inst; q += gridDim.x) {
+    const int64_t p = q >> 1;
+    const int side = (int)(q & 1);
+    const int gid = A.pairs[2 * p + side];
+    const int o = A.node_off[gid];
+    const int N = A.node_off[gid + 1] - o;
+    const int n16 = (N + 15) & ~15;
+    const int ntile = n16 >> 4;
+    const uint32_t pk = sg_pair_key(A.key, (uint32_t)(A.pair_offset + p));
+    const int *__restrict__ rp = A.row_ptr + o;
+    // effective one-hot column per node (sparse dropout of X, layer 0, e = node)
+    for (int n = tid; n < n16; n += 64 * GW)
+      sEt[n] = (n < N && sg_keep(pk, 0, side, n, A.thr0)) ? A.types[o + n] : d_in;
+    __syncthreads();
+
+    // ---- forward: H1 (lane (i, g): node 16t+i, features 16c + 4g + s), D1', Z1 ----
+    for (int t = w; t < ntile; t += GW) {
+      const int n = 16 * t + i;
+      float h[8];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const float4 b = *(const float4 *)(sb0 + 16 * c + 4 * g);
+        h[4 * c] = b.x; h[4 * c + 1] = b.y; h[4 * c + 2] = b.z; h[4 * c + 3] = b.w;
+      }
+      if (n < N) {
+        const int e0 = rp[n], e1 = rp[n + 1];
+        for (int e = e0; e < e1; ++e) {
+          const int mm = A.col[e];
+          const float v = A.val[e];
+          const float *wr = sW0 + sEt[mm] * WH1 + 4 * g;
+          const float4 wa = *(const float4 *)wr, wb = *(const float4 *)(wr + 16);
+          h[0] = fmaf(v, wa.x, h[0]); h[1] = fmaf(v, wa.y, h[1]);
+          h[2] = fmaf(v, wa.z, h[2]); h[3] = fmaf(v, wa.w, h[3]);
+          h[4] = fmaf(v, wb.x, h[4]); h[5] = fmaf(v, wb.y, h[5]);
+          h[6] = fmaf(v, wb.z, h[6]); h[7] = fmaf(v, wb.w, h[7]);
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const int f = 16 * c + 4 * g + s;
+            const float hv = h[4 * c + s] > 0.f ? h[4 * c + s] : 0.f;
+            h[4 * c + s] = sg_keep(pk, 1, side, (uint32_t)(n * WH1 + f), A.thr1) ? hv : 0.f;
+          }
+      } else {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) h[s] = 0.f;
+      }
+      f4 z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) z = mfma4(h[4 * c + s], sW1[(16 * c + 4 * g + s) * WH2 + i], z);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sZ1[(16 * t + 4 * g + r) * WH2 + i] = z[r];
+      if (BWD) {
+        *(float4 *)(sD1 + n * WH1 + 4 * g) = make_float4(h[0], h[1], h[2], h[3]);
+        *(float4 *)(sD1 + n * WH1 + 16 + 4 * g) = make_float4(h[4], h[5], h[6], h[7]);
+      }
+    }
+    __syncthreads();
+
+    // ---- H2 (lane (i, g): node 16t+i, features 4g..4g+3), Dense, Padding, NTN input ----
+    for (int t = w; t < ntile; t += GW) {
+      const int n = 16 * t + i;
+      float h2[4] = {0.f, 0.f, 0.f, 0.f};
+      if (n < N) {
+        const float4 b = *(const float4 *)(sb1 + 4 * g);
+        h2[0] = b.x; h2[1] = b.y; h2[2] = b.z; h2[3] = b.w;
+        const int e0 = rp[n], e1 = rp[n + 1];
+        for (int e = e0; e < e1; ++e) {
+          const int mm = A.col[e];
+          const float v = A.val[e];
+          const float4 zz = *(const float4 *)(sZ1 + mm * WH2 + 4 * g);
+          h2[0] = fmaf(v, zz.x, h2[0]); h2[1] = fmaf(v, zz.y, h2[1]);
+          h2[2] = fmaf(v, zz.z, h2[2]); h2[3] = fmaf(v, zz.w, h2[3]);
+        }
+      }
+      bool k2[4];
+      float part = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        k2[s] = sg_keep(pk, 2, side, (uint32_t)(n * WH2 + 4 * g + s), A.thr2);
+        part = fmaf(k2[s] ? h2[s] : 0.f, sWd[4 * g + s], part);
+      }
+      const float pre = sgk::xsum32(sgk::xsum16(part)) + bd;
+      const float z = pre > 0.f ? pre : 0.f;
+      const bool k4 = n < N && sg_keep(pk, 4, side, (uint32_t)n, A.thr4);
+      if (!BWD) {
+        if (g == 0 && n < N)
+          A.X[((int64_t)side * A.Cp + p) * A.Dp + n] = k4 ? z * A.ik4 : 0.f;
+      } else {
+        // Dense / Padding / NTN-input backward; gZ1 of this node into sG1
+        const float gx = k4 ? A.GX[((int64_t)side * A.Cp + p) * A.Dp + n] * A.ik4 : 0.f;
+        const float gp = (n < N && pre > 0.f) ? gx : 0.f;
+        if (g == 0) aBd += gp;
+        float gz[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          aWd[s] = fmaf(k2[s] ? h2[s] : 0.f, gp, aWd[s]);
+          gz[s] = k2[s] ? gp * sWd[4 * g + s] : 0.f;   // gH2 = gZ1 (identity act)
+          aB1[s] += gz[s];
+        }
+        *(float4 *)(sG1 + n * WH2 + 4 * g) = make_float4(gz[0], gz[1], gz[2], gz[3]);
+      }
+    }
+    if (!BWD) {
+      // Padding rows [N, Dp): padding_value (zero beyond D), after the NTN-input dropout
+      for (int a = N + tid; a < A.Dp; a += 64 * GW)
+        A.X[((int64_t)side * A.Cp + p) * A.Dp + a] =
+            (a < A.D && A.padv != 0.f && sg_keep(pk, 4, side, (uint32_t)a, A.thr4))
+                ? A.padv * A.ik4 : 0.f;
+      __syncthreads();   // sEt / sZ1 are rewritten by the next instance
+      continue;
+    }
+    __syncthreads();
+
+    // ---- gS1 = Â·gZ1 (lane (i, g): node 16t+i, j = 4g..4g+3); gD1 = gS1·W1ᵀ; gW1 ----
+    for (int t = w; t < ntile; t += GW) {
+      const int n = 16 * t + i;
+      float q4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (n < N) {
+        const int e0 = rp[n], e1 = rp[n + 1];
+        for (int e = e0; e < e1; ++e) {
+          const int mm = A.col[e];
+          const float v = A.val[e];
+          const float4 gg = *(const float4 *)(sG1 + mm * WH2 + 4 * g);
+          q4[0] = fmaf(v, gg.x, q4[0]); q4[1] = fmaf(v, gg.y, q4[1]);
+          q4[2] = fmaf(v, gg.z, q4[2]); q4[3] = fmaf(v, gg.w, q4[3]);
+        }
+      }
+      // gD1·ik1 (rows n = 16t + 4g + r, column f = 16cb + i)
+      f4 gd[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) gd[cb] = mfma4(q4[s], sW1T[(4 * g + s) * WH1 + 16 * cb + i], gd[cb]);
+      // gS1 of this tile into sZ1 (dead: every wave passed the H2 loop), read back as B
+      *(float4 *)(sZ1 + n * WH2 + 4 * g) = make_float4(q4[0], q4[1], q4[2], q4[3]);
+      sg_wsync();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int nn = 16 * t + 4 * g + s;
+        const float b = sZ1[nn * WH2 + i];
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) aW1[cb] = mfma4(sD1[nn * WH1 + 16 * cb + i], b, aW1[cb]);
+      }
+      sg_wsync();
+      // gP0 = relu'·keep·gD1·ik1 = (D1' > 0) · gD1·ik1, in place of D1'
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float *dp = sD1 + (16 * t + 4 * g + r) * WH1 + 16 * cb + i;
+          const float v = *dp > 0.f ? gd[cb][r] : 0.f;
+          aB0[cb] += v;
+          *dp = v;
+        }
+    }
+    __syncthreads();
+
+    // ---- gS0 = Â·gP0 (rows n = 16t + 4g + s, features i, 16 + i); gW0 += Xᵀ·(scale0·gS0) ----
+    for (int t = w; t < ntile; t += GW) {
+      float bq[4][2];
+      int et[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int n = 16 * t + 4 * g + s;
+        float q0 = 0.f, q1 = 0.f;
+        et[s] = sEt[n];
+        if (n < N && et[s] < d_in) {
+          const int e0 = rp[n], e1 = rp[n + 1];
+          for (int e = e0; e < e1; ++e) {
+            const int mm = A.col[e];
+            const float v = A.val[e];
+            q0 = fmaf(v, sD1[mm * WH1 + i], q0);
+            q1 = fmaf(v, sD1[mm * WH1 + 16 + i], q1);
+          }
+        }
+        bq[s][0] = q0 * A.ik0;   // scale0 = keep0 · ik0 (dropped nodes: et = d_in, q = 0)
+        bq[s][1] = q1 * A.ik0;
+      }
+#pragma unroll
+      for (int tb = 0; tb < NTB; ++tb)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const float a = et[s] == 16 * tb + i ? 1.f : 0.f;
+          aW0[tb][0] = mfma4(a, bq[s][0], aW0[tb][0]);
+          aW0[tb][1] = mfma4(a, bq[s][1], aW0[tb][1]);
+        }
+    }
+    __syncthreads();   // sD1 / sEt are rewritten by the next instance
+  }
+  if (!BWD) return;
+
+  // ---- flush: each wave writes its gradient contributions into its own LDS row,
+  // then the block sums the waves in order into its slab row (deterministic) ----
+  const int C = A.n_gcn;
+  float *row = sm + L.tables + w * C;   // the instance region is dead
+  for (int x = l; x < C; x += 64) row[x] = 0.f;
+  sg_wsync();
+#pragma unroll
+  for (int tb = 0; tb < NTB; ++tb)
+#pragma unroll
+    for (int fb = 0; fb < 2; ++fb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ty = 16 * tb + 4 * g + r;
+        if (ty < d_in) row[ty * WH1 + 16 * fb + i] = aW0[tb][fb][r];
+      }
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const float v = sgk::xsum32(sgk::xsum16(aB0[cb]));
+    if (g == 0) row[A.ob0 + 16 * cb + i] = v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) row[A.oW1 + (16 * cb + 4 * g + r) * WH2 + i] = aW1[cb][r] * A.ik1;
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const float vb = sgk::row_sum16(aB1[s]);
+    const float vd = sgk::row_sum16(aWd[s]) * A.ik2;
+    if (i == 0) {
+      row[A.ob1 + 4 * g + s] = vb;
+      row[A.oWd + 4 * g + s] = vd;
+    }
+  }
+  const float bsum = sg_wave_sum(aBd);
+  if (l == 0) row[A.obd] = bsum;
+  __syncthreads();
+  float *dst = A.slab + (size_t)blockIdx.x * C;
+  for (int x = tid; x < C; x += 64 * GW) {
+    float v = 0.f;
+    for (int u = 0; u < GW; ++u) v += sm[L.tables + u * C + x];
+    dst[x] += v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 128×128 f32 MFMA GEMM tiles (4 waves as 2×2, 64×64 per wave).
+// MK layout: rows m, 16 contraction values + pad (one b128 read per 4 k-steps with
+// the k-step order kk = 4g + s); KM layout: 16 contraction rows × 128 (+4).
+// ---------------------------------------------------------------------------
+struct Tile {
+  f4 c[4][4];
+  __device__ void zero() {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) c[a][b] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+};
+
+__device__ __forceinline__ void mma_mk_mk(Tile &T, const float *sA, const float *sB, int wm,
+                                          int wn, int i, int g) {
+  float4 a[4], b[4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    a[x] = *(const float4 *)(sA + (wm * 64 + x * 16 + i) * MKS + 4 * g);
+    b[x] = *(const float4 *)(sB + (wn * 64 + x * 16 + i) * MKS + 4 * g);
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const float av = s == 0 ? a[mi].x : s == 1 ? a[mi].y : s == 2 ? a[mi].z : a[mi].w;
+        const float bv = s == 0 ? b[ni].x : s == 1 ? b[ni].y : s == 2 ? b[ni].z : b[ni].w;
+        T.c[mi][ni] = mfma4(av, bv, T.c[mi][ni]);
+      }
+}
+
+__device__ __forceinline__ void mma_km_km(Tile &T, const float *sA, const float *sB, int wm,
+                                          int wn, int i, int g) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    float a[4], b[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      a[x] = sA[(4 * g + s) * KMS + wm * 64 + x * 16 + i];
+      b[x] = sB[(4 * g + s) * KMS + wn * 64 + x * 16 + i];
+    }
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) T.c[mi][ni] = mfma4(a[mi], b[ni], T.c[mi][ni]);
+  }
+}
+
+// ---- T[p][k][a] = Σ_b W[a][b][k] x2[p][b]  (grid: p-blocks × a-tiles × k) ----
+__global__ void __launch_bounds__(256) web_t_kernel(const float *__restrict__ X2,
+                                                    const float *__restrict__ Wg,
+                                                    const int2 *__restrict__ ext128, int64_t n,
+                                                    int Dp, int K, float *__restrict__ Tout) {
+  __shared__ __attribute__((aligned(16))) float sA[TB * MKS], sB[TB * MKS];
+  const int64_t p0 = (int64_t)blockIdx.x * TB;
+  const int a0 = blockIdx.y * TB, k = blockIdx.z;
+  const int2 e = ext128[blockIdx.x];
+  if (a0 >= e.x) return;
+  const int nb = (e.y + 15) & ~15;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, i = l & 15, g = l >> 4;
+  const int wm = w >> 1, wn = w & 1;
+  const float *pa = X2 + p0 * Dp;
+  const float *pb = Wg + ((size_t)k * Dp + a0) * Dp;
+  float4 ra[2], rb[2];
+  auto load = [&](int b0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = tid + 256 * u, r = q >> 2, sg = (q & 3) * 4;
+      ra[u] = *(const float4 *)(pa + (size_t)r * Dp + b0 + sg);
+      rb[u] = *(const float4 *)(pb + (size_t)r * Dp + b0 + sg);
+    }
+  };
+  Tile T;
+  T.zero();
+  if (nb > 0) load(0);
+  for (int b0 = 0; b0 < nb; b0 += 16) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = tid + 256 * u, r = q >> 2, sg = (q & 3) * 4;
+      *(float4 *)(sA + r * MKS + sg) = ra[u];
+      *(float4 *)(sB + r * MKS + sg) = rb[u];
+    }
+    __syncthreads();
+    if (b0 + 16 < nb) load(b0 + 16);
+    mma_mk_mk(T, sA, sB, wm, wn, i, g);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t p = p0 + wm * 64 + mi * 16 + 4 * g + r;
+      if (p >= n) continue;
+      float *dst = Tout + ((size_t)p * K + k) * Dp + a0 + wn * 64 + i;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) dst[ni * 16] = T.c[mi][ni][r];
+    }
+}
+
+// ---- gX2[p][b] += Σ_{k,a} gm[p][k] x1[p][a] W[a][b][k]  (grid: p-blocks × b-tiles) ----
+__global__ void __launch_bounds__(256) web_gx2_kernel(const float *__restrict__ X1,
+                                                      const float *__restrict__ GM,
+                                                      const float *__restrict__ Wh,
+                                                      const int2 *__restrict__ ext128, int64_t n,
+                                                      int Dp, int K, float *__restrict__ GX2) {
+  __shared__ __attribute__((aligned(16))) float sA[TB * MKS], sB[TB * MKS];
+  const int64_t p0 = (int64_t)blockIdx.x * TB;
+  const int b0 = blockIdx.y * TB;
+  const int2 e = ext128[blockIdx.x];
+  if (b0 >= e.y) return;
+  const int na = (e.x + 15) & ~15;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, i = l & 15, g = l >> 4;
+  const int wm = w >> 1, wn = w & 1;
+  float4 ra[2], rb[2];
+  float gmr[2];
+  auto load = [&](int k, int a0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = tid + 256 * u, r = q >> 2, sg = (q & 3) * 4;
+      const int64_t p = p0 + r;
+      gmr[u] = p < n ? GM[p * WKP + k] : 0.f;
+      ra[u] = *(const float4 *)(X1 + p * Dp + a0 + sg);
+      rb[u] = *(const float4 *)(Wh + ((size_t)k * Dp + b0 + r) * Dp + a0 + sg);
+    }
+  };
+  Tile T;
+  T.zero();
+  const int steps = na / 16, total = K * steps;
+  if (total > 0) load(0, 0);
+  for (int st = 0; st < total; ++st) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = tid + 256 * u, r = q >> 2, sg = (q & 3) * 4;
+      const float gm = gmr[u];
+      *(float4 *)(sA + r * MKS + sg) =
+          make_float4(gm * ra[u].x, gm * ra[u].y, gm * ra[u].z, gm * ra[u].w);
+      *(float4 *)(sB + r * MKS + sg) = rb[u];
+    }
+    __syncthreads();
+    if (st + 1 < total) load((st + 1) / steps, ((st + 1) % steps) * 16);
+    mma_mk_mk(T, sA, sB, wm, wn, i, g);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t p = p0 + wm * 64 + mi * 16 + 4 * g + r;
+      if (p >= n) continue;
+      float *dst = GX2 + p * Dp + b0 + wn * 64 + i;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) dst[ni * 16] += T.c[mi][ni][r];
+    }
+}
+
+// ---- gWs[s][k][a][b] += Σ_{p in split s} gm[p][k] x1[p][a] x2[p][b]
+//      (grid: a-tile·b-tile × k × split) ----
+__global__ void __launch_bounds__(256) web_wgrad_kernel(const float *__restrict__ X1,
+                                                        const float *__restrict__ X2,
+                                                        const float *__restrict__ GM,
+                                                        const int2 *__restrict__ ext16, int64_t n,
+                                                        int Dp, int K, float *__restrict__ GWS) {
+  __shared__ __attribute__((aligned(16))) float sA[16 * KMS], sB[16 * KMS];
+  const int nbt = Dp / TB;
+  const int a0 = (blockIdx.x / nbt) * TB, b0 = (blockIdx.x % nbt) * TB;
+  const int k = blockIdx.y, s = blockIdx.z;
+  const int64_t nc = (n + 15) / 16;   // 16-pair chunks of the batch
+  const int64_t c0 = nc * s / WSPLIT, c1 = nc * (s + 1) / WSPLIT;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, i = l & 15, g = l >> 4;
+  const int wm = w >> 1, wn = w & 1;
+  Tile T;
+  T.zero();
+  for (int64_t c = c0; c < c1; ++c) {
+    const int2 e = ext16[c];
+    if (e.x <= a0 || e.y <= b0) continue;   // every pair of the chunk is zero on this tile
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = tid + 256 * u, r = q >> 5, cc = (q & 31) * 4;
+      const int64_t p = c * 16 + r;
+      float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+      if (p < n) {
+        const float gm = GM[p * WKP + k];
+        const float4 x = *(const float4 *)(X1 + p * Dp + a0 + cc);
+        va = make_float4(gm * x.x, gm * x.y, gm * x.z, gm * x.w);
+        vb = *(const float4 *)(X2 + p * Dp + b0 + cc);
+      }
+      *(float4 *)(sA + r * KMS + cc) = va;
+      *(float4 *)(sB + r * KMS + cc) = vb;
+    }
+    __syncthreads();
+    mma_km_km(T, sA, sB, wm, wn, i, g);
+    __syncthreads();
+  }
+  float *base = GWS + (((size_t)s * K + k) * Dp) * Dp;
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int a = a0 + wm * 64 + mi * 16 + 4 * g + r;
+      float *dst = base + (size_t)a * Dp + b0 + wn * 64 + i;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) dst[ni * 16] += T.c[mi][ni][r];
+    }
+}
+
+// ---- gVs[s][k][c] += Σ_{p in split s} gm[p][k] x12[p][c]  (c < Dp: x1, else x2) ----
+__global__ void __launch_bounds__(256) web_gv_kernel(const float *__restrict__ X,
+                                                     const float *__restrict__ GM, int64_t n,
+                                                     int64_t Cp, int Dp, int K,
+                                                     float *__restrict__ GVS) {
+  __shared__ float red[4][WKP][64];
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int c = blockIdx.x * 64 + l, s = blockIdx.y;
+  const int64_t q0 = n * s / WSPLIT, q1 = n * (s + 1) / WSPLIT;
+  const float *src = c < Dp ? X + c : X + Cp * Dp + (c - Dp);
+  float acc[WKP];
+#pragma unroll
+  for (int k = 0; k < WKP; ++k) acc[k] = 0.f;
+  for (int64_t p = q0 + w; p < q1; p += 4) {
+    const float x = src[p * Dp];
+    const float4 *gm4 = (const float4 *)(GM + p * WKP);
+#pragma unroll
+    for (int k4 = 0; k4 < WKP / 4; ++k4) {
+      const float4 gm = gm4[k4];
+      acc[4 * k4] = fmaf(gm.x, x, acc[4 * k4]);
+      acc[4 * k4 + 1] = fmaf(gm.y, x, acc[4 * k4 + 1]);
+      acc[4 * k4 + 2] = fmaf(gm.z, x, acc[4 * k4 + 2]);
+      acc[4 * k4 + 3] = fmaf(gm.w, x, acc[4 * k4 + 3]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < WKP; ++k) red[w][k][l] = acc[k];
+  __syncthreads();
+  for (int x = tid; x < K * 64; x += 256) {
+    const int k = x >> 6, cl = x & 63;
+    const float v = (red[0][k][cl] + red[1][k][cl]) + (red[2][k][cl] + red[3][k][cl]);
+    GVS[((size_t)s * WKP + k) * 2 * Dp + blockIdx.x * 64 + cl] += v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Per-pair NTN head: m_k, s, ŷ, loss, gm; gx1 = Σ_k gm_k (T_k + V_k),
+// gx2 := Σ_k gm_k V_k[D + ·] (web_gx2 adds the W term).  One wave per pair.
+// ---------------------------------------------------------------------------
+struct HeadArgs {
+  const float *X, *T, *params, *labels, *y_stats;
+  const int2 *ext;
+  float *GX, *GM, *s_out, *hslab;
+  int64_t n, Cp;
+  int D, Dp, K, oV, oU, obn;
+  int final_act, loss_mode, ntn_mode;
+  float yeta, inv_batch;
+};
+
+template <bool BWD>
+__global__ void __launch_bounds__(256) web_head_kernel(HeadArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float sV[];   // [K][2Dp]: V[k][a] | V[k][D+b]
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int D = A.D, Dp = A.Dp, K = A.K;
+  for (int x = tid; x < K * 2 * Dp; x += 256) {
+    const int k = x / (2 * Dp), c = x % (2 * Dp);
+    const int cc = c < Dp ? c : c - Dp;
+    sV[x] = cc < D ? A.params[A.oV + k * 2 * D + (c < Dp ? 0 : D) + cc] : 0.f;
+  }
+  float U[WKP], bn[WKP];
+  float usum = 0.f;
+#pragma unroll
+  for (int k = 0; k < WKP; ++k) {
+    U[k] = k < K ? A.params[A.oU + k] : 0.f;
+    bn[k] = (k < K && A.obn >= 0) ? A.params[A.obn + k] : 0.f;
+    usum += U[k];
+  }
+  const float ybar = (A.loss_mode == SG_LOSS_BROADCAST && A.y_stats) ? A.y_stats[0] : 0.f;
+  __syncthreads();
+  const int nc = Dp / 64;
+  float aLoss = 0.f, aU = 0.f, aB = 0.f;   // lane k: gU[k], gb[k]
+  const int64_t gw = (int64_t)blockIdx.x * 4 + w, nw = (int64_t)gridDim.x * 4;
+  for (int64_t p = gw; p < A.n; p += nw) {
+    const int e1 = A.ext[p].x;
+    const float *x1 = A.X + p * Dp, *x2 = A.X + (A.Cp + p) * Dp;
+    const float *Tp = A.T + (size_t)p * K * Dp;
+    float m[WKP];
+#pragma unroll
+    for (int k = 0; k < WKP; ++k) m[k] = 0.f;
+    for (int c = 0; c < nc; ++c) {
+      const int a = 64 * c + l;
+      const float xa = x1[a], xb = x2[a];
+#pragma unroll
+      for (int k = 0; k < WKP; ++k) {
+        if (k < K) {
+          const float t = a < e1 ? Tp[k * Dp + a] : 0.f;
+          m[k] = fmaf(xa, t + sV[k * 2 * Dp + a], m[k]);
+          m[k] = fmaf(xb, sV[k * 2 * Dp + Dp + a], m[k]);
+        }
+      }
+    }
+    float rsum = 0.f, s = 0.f;
+#pragma unroll
+    for (int k = 0; k < WKP; ++k) {
+      if (k < K) {
+        m[k] = sg_wave_sum(m[k]) + bn[k];
+        const float r = m[k] > 0.f ? m[k] : 0.f;
+        rsum += r;
+        s = fmaf(U[k], r, s);
+      }
+    }
+    if (A.ntn_mode == SG_NTN_REFERENCE) s = usum * rsum;   // quirk A1
+    if (!BWD) {
+      if (l == 0 && A.s_out) A.s_out[p] = s;
+      continue;
+    }
+    const float yh = sg_final(A.final_act, A.yeta, s);
+    float gy;
+    if (A.loss_mode == SG_LOSS_BROADCAST) {
+      gy = yh - ybar;                       // quirk A2: ∂/∂ŷ_j = ŷ_j - ȳ
+      aLoss += 0.5f * gy * gy;
+    } else {
+      const float y = A.labels[p];
+      gy = (yh - y) * A.inv_batch;
+      aLoss += 0.5f * (y - yh) * (y - yh) * A.inv_batch;
+    }
+    const float gs = gy * sg_final_grad(A.final_act, A.yeta, s, yh);
+    float gm[WKP];
+#pragma unroll
+    for (int k = 0; k < WKP; ++k) {
+      const float gr = A.ntn_mode == SG_NTN_REFERENCE ? gs * usum : gs * U[k];
+      gm[k] = (k < K && m[k] > 0.f) ? gr : 0.f;
+      if (l == k) {
+        aU += A.ntn_mode == SG_NTN_REFERENCE ? gs * rsum : gs * (m[k] > 0.f ? m[k] : 0.f);
+        aB += gm[k];
+      }
+    }
+    if (l < WKP) {
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < WKP; ++k) v = l == k ? gm[k] : v;
+      A.GM[p * WKP + l] = v;
+    }
+    if (l == 0 && A.s_out) A.s_out[p] = s;
+    float *g1 = A.GX + p * Dp, *g2 = A.GX + (A.Cp + p) * Dp;
+    for (int c = 0; c < nc; ++c) {
+      const int a = 64 * c + l;
+      float v1 = 0.f, v2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < WKP; ++k) {
+        if (k < K) {
+          const float t = a < e1 ? Tp[k * Dp + a] : 0.f;
+          v1 = fmaf(gm[k], t + sV[k * 2 * Dp + a], v1);
+          v2 = fmaf(gm[k], sV[k * 2 * Dp + Dp + a], v2);
+        }
+      }
+      g1[a] = v1;
+      g2[a] = v2;
+    }
+  }
+  if (!BWD) return;
+  float *row = A.hslab + ((size_t)blockIdx.x * 4 + w) * HSLAB;
+  if (l == 0) row[0] += aLoss;   // wave-uniform
+  if (l < WKP) {
+    row[1 + l] += aU;
+    row[1 + WKP + l] += aB;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Final reductions (once per call): column sums in fixed order.
+// ---------------------------------------------------------------------------
+// dst[c] = Σ_r src[r·stride + c] (+ add[0] on column `addcol`)
+__global__ void __launch_bounds__(1024) web_colsum(const float *__restrict__ src, int rows,
+                                                   int cols, int stride, float *__restrict__ dst,
+                                                   int dstride, const float *__restrict__ add,
+                                                   int addcol) {
+  __shared__ float red[16][64];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + l;
+  float a0 = 0.f, a1 = 0.f;
+  if (c < cols)
+    for (int r = w; r < rows; r += 32) {
+      a0 += src[(size_t)r * stride + c];
+      if (r + 16 < rows) a1 += src[(size_t)(r + 16) * stride + c];
+    }
+  red[w][l] = a0 + a1;
+  __syncthreads();
+  if (w == 0 && c < cols) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += red[k][l];
+    if (add && c == addcol) v += add[0];
+    dst[(size_t)c * dstride] = v;
+  }
+}
+
+// grad W[a][b][k] = Σ_s gWs[s][k][a][b]   (block: row a, 64 b's, all k)
+__global__ void __launch_bounds__(256) web_wsum(const float *__restrict__ GWS, int D, int Dp, int K,
+                                                float *__restrict__ gW) {
+  __shared__ float t[64 * (WKP + 1)];
+  const int a = blockIdx.x, b0 = blockIdx.y * 64;
+  for (int x = threadIdx.x; x < 64 * K; x += 256) {
+    const int k = x >> 6, bl = x & 63;
+    float v = 0.f;
+    for (int s = 0; s < WSPLIT; ++s) v += GWS[(((size_t)s * K + k) * Dp + a) * Dp + b0 + bl];
+    t[bl * (WKP + 1) + k] = v;
+  }
+  __syncthreads();
+  const int nb = min(64, D - b0);
+  for (int x = threadIdx.x; x < nb * K; x += 256) {
+    const int bl = x / K, k = x % K;
+    gW[((size_t)a * D + b0 + bl) * K + k] = t[bl * (WKP + 1) + k];
+  }
+}
+
+// grad V[k][c] = Σ_s gVs[s][k][c'] (c < D: c' = c; else c' = Dp + c - D)
+__global__ void __launch_bounds__(256) web_vsum(const float *__restrict__ GVS, int D, int Dp, int K,
+                                                float *__restrict__ gV) {
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  if (x >= K * 2 * D) return;
+  const int k = x / (2 * D), c = x % (2 * D);
+  const int cc = c < D ? c : Dp + c - D;
+  float v = 0.f;
+  for (int s = 0; s < WSPLIT; ++s) v += GVS[((size_t)s * WKP + k) * 2 * Dp + cc];
+  gV[x] = v;
+}
+
+__global__ void web_copy_scalar(const float *__restrict__ src, float *__restrict__ dst) {
+  if (threadIdx.x == 0) dst[0] = src[0];
+}
+
+}  // namespace
+
+// ===========================================================================
+// Host side
+// ===========================================================================
+int sg_web_plan_params(const sg_model_t *m, int64_t *n_params) {
+  WebPlan W;
+  const int rc = web_plan(m, &W);
+  if (rc == SG_OK && n_params) *n_params = W.n_params;
+  return rc;
+}
+
+int64_t sg_web_ws_bytes(const sg_model_t *m, int64_t chunk) {
+  WebPlan W;
+  if (web_plan(m, &W) != SG_OK) return -1;
+  return web_ws(W, chunk).total * 4 + 256;
+}
+
+static int web_status() {
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess) return SG_OK;
+  if (getenv("SG_DEBUG")) fprintf(stderr, "sg_web: %s\n", hipGetErrorString(e));
+  return SG_ERR_HIP;
+}
+
+static void gcn_launch(bool bwd, const WebPlan &W, const GcnArgs &A, int blocks, hipStream_t st) {
+  const int n16 = (A.n_max + 15) & ~15;
+  const GcnLds L = gcn_lds(W.d_in, n16, bwd);
+  size_t lds = (size_t)L.total * 4u;
+  if (bwd) {
+    const size_t fl = ((size_t)L.tables + (size_t)GW * W.n_gcn) * 4u;
+    if (fl > lds) lds = fl;
+  }
+  const void *fn = nullptr;
+#define SG_WEB_GCN(B, NT)                                                                      \
+  do {                                                                                       \
+    fn = (const void *)web_gcn_kernel<B, NT>;                                                \
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);     \
+    hipLaunchKernelGGL((web_gcn_kernel<B, NT>), dim3(blocks), dim3(64 * GW), lds, st, A);    \
+  } while (0)
+  switch (W.tb) {
+    case 1: if (bwd) SG_WEB_GCN(true, 1); else SG_WEB_GCN(false, 1); break;
+    case 2: if (bwd) SG_WEB_GCN(true, 2); else SG_WEB_GCN(false, 2); break;
+    case 3: if (bwd) SG_WEB_GCN(true, 3); else SG_WEB_GCN(false, 3); break;
+    default: if (bwd) SG_WEB_GCN(true, 4); else SG_WEB_GCN(false, 4); break;
+  }
+#undef SG_WEB_GCN
+}
+
+int sg_web_lds_ok(const sg_model_t *m) {
+  WebPlan W;
+  if (web_plan(m, &W) != SG_OK) return 0;
+  const int n16 = (m->n_max + 15) & ~15;
+  const GcnLds L = gcn_lds(W.d_in, n16, true);
+  const size_t fl = ((size_t)L.tables + (size_t)GW * W.n_gcn) * 4u;
+  return (size_t)L.total * 4u <= 163840u && fl <= 163840u;
+}
+
+int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *pairs,
+               const float *labels, int64_t n_pairs, int64_t pair_offset, int64_t batch_total,
+               const float *params, uint64_t seed, const float *y_stats, int add_label,
+               float *s_out, float *grad_out, float *loss_out, void *workspace, int64_t chunk,
+               bool bwd, hipStream_t st) {
+  WebPlan W;
+  int rc = web_plan(m, &W);
+  if (rc != SG_OK) return rc;
+  if (!store || !store->node_off || !store->types || !store->row_ptr || !store->col ||
+      !store->val || store->n_max > W.D || store->n_max > m->n_max)
+    return SG_ERR_ARG;
+  if (!sg_web_lds_ok(m)) return SG_ERR_UNSUPPORTED;
+  if (chunk <= 0) chunk = n_pairs > 0 ? n_pairs : 1;
+  (void)hipGetLastError();   // report only this call's launch errors
+  const WebWs ws = web_ws(W, chunk);
+  float *base = (float *)workspace;
+  float *X = base + ws.X, *GX = base + ws.GX, *T = base + ws.T, *GM = base + ws.GM;
+  int2 *EXT = (int2 *)(base + ws.EXT), *EXT16 = (int2 *)(base + ws.EXT16);
+  int2 *EXT128 = (int2 *)(base + ws.EXT128);
+  float *Wg = base + ws.Wg, *Wh = base + ws.Wh, *GWS = base + ws.GWS, *GVS = base + ws.GVS;
+  float *GSLAB = base + ws.GSLAB, *HS = base + ws.HSLABo;
+  const int Dp = W.Dp, K = W.K, D = W.D;
+
+  if (bwd) {
+    if (hipMemsetAsync(GWS, 0, (size_t)WSPLIT * K * Dp * Dp * 4u, st) != hipSuccess ||
+        hipMemsetAsync(GVS, 0, (size_t)WSPLIT * WKP * 2 * Dp * 4u, st) != hipSuccess ||
+        hipMemsetAsync(GSLAB, 0, (size_t)ws.gcn_blocks * W.n_gcn * 4u, st) != hipSuccess ||
+        hipMemsetAsync(HS, 0, (size_t)ws.head_blocks * 4 * HSLAB * 4u, st) != hipSuccess)
+      return SG_ERR_HIP;
+  }
+  if (n_pairs > 0) {
+    hipLaunchKernelGGL(web_wprep_g, dim3(Dp, Dp / 64), dim3(256), 0, st, params + W.oW, D, Dp, K,
+                       Wg);
+    if (bwd)
+      hipLaunchKernelGGL(web_wprep_h, dim3(Dp / 32, Dp / 32, K), dim3(256), 0, st, Wg, Dp, Wh);
+  }
+  GcnArgs G;
+  G.node_off = store->node_off;
+  G.types = store->types;
+  G.row_ptr = store->row_ptr;
+  G.col = store->col;
+  G.val = store->val;
+  G.Cp = ws.Cp;
+  G.params = params;
+  G.X = X;
+  G.GX = GX;
+  G.slab = GSLAB;
+  G.key = sg_seed_key(seed);
+  G.thr0 = W.thr0; G.thr1 = W.thr1; G.thr2 = W.thr2; G.thr4 = W.thr4;
+  G.ik0 = W.ik0; G.ik1 = W.ik1; G.ik2 = W.ik2; G.ik4 = W.ik4;
+  G.padv = W.padv;
+  G.d_in = W.d_in; G.D = D; G.Dp = Dp; G.n_gcn = W.n_gcn; G.n_max = store->n_max;
+  G.ob0 = W.ob0; G.oW1 = W.oW1; G.ob1 = W.ob1; G.oWd = W.oWd; G.obd = W.obd;
+  HeadArgs H;
+  H.X = X; H.T = T; H.params = params; H.labels = labels; H.y_stats = y_stats;
+  H.ext = EXT; H.GX = GX; H.GM = GM; H.s_out = nullptr; H.hslab = HS;
+  H.Cp = ws.Cp; H.D = D; H.Dp = Dp; H.K = K; H.oV = W.oV; H.oU = W.oU; H.obn = W.obn;
+  H.final_act = W.final_act; H.loss_mode = W.loss_mode; H.ntn_mode = W.ntn_mode;
+  H.yeta = W.yeta;
+  H.inv_batch = batch_total > 0 ? 1.f / (float)batch_total : 0.f;
+  const size_t head_lds = (size_t)K * 2 * Dp * 4u;
+  const int full = W.padv != 0.f ? 1 : 0;
+
+  for (int64_t c0 = 0; c0 < n_pairs; c0 += chunk) {
+    const int64_t n = n_pairs - c0 < chunk ? n_pairs - c0 : chunk;
+    const int64_t nblk = (n + TB - 1) / TB;
+    const int32_t *pc = pairs + 2 * c0;
+    hipLaunchKernelGGL(web_ext_kernel, dim3((unsigned)nblk), dim3(TB), 0, st, pc, n,
+                       store->node_off, full, D, EXT, EXT16, EXT128);
+    G.pairs = pc;
+    G.n_pairs = n;
+    G.pair_offset = pair_offset + c0;
+    const int64_t gb = 2 * n < ws.gcn_blocks ? 2 * n : ws.gcn_blocks;
+    gcn_launch(false, W, G, (int)gb, st);
+    hipLaunchKernelGGL(web_t_kernel, dim3((unsigned)nblk, Dp / TB, K), dim3(256), 0, st,
+                       X + ws.Cp * Dp, Wg,
+                       EXT128, n, Dp, K, T);
+    H.n = n;
+    H.labels = labels ? labels + c0 : nullptr;
+    H.s_out = s_out ? s_out + c0 : nullptr;
+    const int hb = (int)((n + 3) / 4 < ws.head_blocks ? (n + 3) / 4 : ws.head_blocks);
+    if (bwd) {
+      hipLaunchKernelGGL(web_head_kernel<true>, dim3(hb), dim3(256), head_lds, st, H);
+      hipLaunchKernelGGL(web_gx2_kernel, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, st, X, GM,
+                         Wh, EXT128, n, Dp, K, GX + ws.Cp * Dp);
+      hipLaunchKernelGGL(web_wgrad_kernel, dim3((Dp / TB) * (Dp / TB), K, WSPLIT), dim3(256), 0,
+                         st, X, X + ws.Cp * Dp, GM, EXT16, n, Dp, K, GWS);
+      hipLaunchKernelGGL(web_gv_kernel, dim3(2 * Dp / 64, WSPLIT), dim3(256), 0, st, X, GM, n,
+                         ws.Cp, Dp, K, GVS);
+      gcn_launch(true, W, G, ws.gcn_blocks, st);
+    } else {
+      hipLaunchKernelGGL(web_head_kernel<false>, dim3(hb), dim3(256), head_lds, st, H);
+    }
+  }
+  if (!bwd) return web_status();
+
+  // gradient assembly in the reference's variable order
+  hipLaunchKernelGGL(web_colsum, dim3((W.n_gcn + 63) / 64), dim3(1024), 0, st, GSLAB,
+                     ws.gcn_blocks, W.n_gcn, W.n_gcn, grad_out, 1, (const float *)nullptr, -1);
+  hipLaunchKernelGGL(web_wsum, dim3(D, Dp / 64), dim3(256), 0, st, GWS, D, Dp, K,
+                     grad_out + W.oW);
+  hipLaunchKernelGGL(web_vsum, dim3((K * 2 * D + 255) / 256), dim3(256), 0, st, GVS, D, Dp, K,
+                     grad_out + W.oV);
+  const int hrows = ws.head_blocks * 4;
+  hipLaunchKernelGGL(web_colsum, dim3(1), dim3(1024), 0, st, HS + 1, hrows, K, HSLAB,
+                     grad_out + W.oU, 1, (const float *)nullptr, -1);
+  if (W.obn >= 0)
+    hipLaunchKernelGGL(web_colsum, dim3(1), dim3(1024), 0, st, HS + 1 + WKP, hrows, K, HSLAB,
+                       grad_out + W.obn, 1, (const float *)nullptr, -1);
+  if (loss_out) {
+    const bool lab = add_label && m->loss_mode == SG_LOSS_BROADCAST && y_stats;
+    hipLaunchKernelGGL(web_colsum, dim3(1), dim3(1024), 0, st, HS, hrows, 1, HSLAB, loss_out, 1,
+                       lab ? y_stats + 1 : (const float *)nullptr, 0);
+  }
+  return web_status();
+}

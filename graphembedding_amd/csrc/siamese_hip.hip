@@ -38,6 +38,15 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
                 hipStream_t stream);
 // fused capacity-32 path (sg_fast32.hip)
 int sg_fast32_supported(const sg_model_t *m, const SgGenPlan &P);
+// graph-store path for Web-sized graphs (sg_web.hip)
+int sg_web_plan_params(const sg_model_t *m, int64_t *n_params);
+int sg_web_lds_ok(const sg_model_t *m);
+int64_t sg_web_ws_bytes(const sg_model_t *m, int64_t chunk);
+int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *pairs,
+               const float *labels, int64_t n_pairs, int64_t pair_offset, int64_t batch_total,
+               const float *params, uint64_t seed, const float *y_stats, int add_label,
+               float *s_out, float *grad_out, float *loss_out, void *workspace, int64_t chunk,
+               bool bwd, hipStream_t st);
 int64_t sg_fast32_slab_floats(const SgGenPlan &P, int64_t n_pairs);
 int64_t sg_fast32_ntn_floats(int64_t n_pairs);
 int sg_fast32_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
@@ -368,6 +377,52 @@ __global__ void __launch_bounds__(1024) sg_adam_kernel(float *__restrict__ th, f
   }
 }
 
+// Multi-block ApplyAdam for large parameter vectors (config C5: 2.6 M parameters):
+// pass 1 updates θ, m, v and writes one Σθ² partial (double) per block; pass 2 sums
+// the partials in order and advances the β powers.
+constexpr int kAdamBlocks = 512;
+__global__ void __launch_bounds__(256) sg_adam_multi(float *__restrict__ th, float *__restrict__ m,
+                                                    float *__restrict__ v,
+                                                    const float *__restrict__ g, int64_t n,
+                                                    float lr, float b1, float b2, float eps,
+                                                    float wd, const float *__restrict__ bp,
+                                                    double *__restrict__ part) {
+  __shared__ double red[4];
+  const float alpha = lr * sqrtf(1.f - bp[1]) / (1.f - bp[0]);
+  const float c1 = 1.f - b1, c2 = 1.f - b2;
+  double reg = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float tv = th[i];
+    reg += (double)tv * (double)tv;
+    const float gi = g[i] + wd * tv;
+    const float mi = m[i] + (gi - m[i]) * c1;
+    const float vi = v[i] + (gi * gi - v[i]) * c2;
+    m[i] = mi;
+    v[i] = vi;
+    th[i] = tv - (mi * alpha) / (sqrtf(vi) + eps);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) reg += __shfl_xor(reg, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = reg;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void __launch_bounds__(64) sg_adam_final(const double *__restrict__ part, int nb,
+                                                   float b1, float b2, float wd,
+                                                   float *__restrict__ bp,
+                                                   float *__restrict__ reg_loss) {
+  double v = 0.0;
+  for (int b = threadIdx.x; b < nb; b += 64) v += part[b];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if (threadIdx.x == 0) {
+    bp[0] *= b1;
+    bp[1] *= b2;
+    if (reg_loss) reg_loss[0] = (float)((double)wd * 0.5 * v);
+  }
+}
+
 int launch_reduce(const float *slab, int nblk, int C, float *part, float *grad, float *loss,
                   const float *y_stats, int add_label, hipStream_t st) {
   if (nblk <= kOnePassRows) {   // the fused kernel's one-block-per-CU slabs
@@ -432,7 +487,7 @@ int64_t ntn_offset_floats(const PathChoice &c, int64_t n_pairs) {
 // ===========================================================================
 extern "C" {
 
-int32_t sg_version(void) { return 10300; }   /* 1.3.0: fused capacity-32 path */
+int32_t sg_version(void) { return 10500; }   /* 1.5.0: graph-store path (config C5) */
 
 int64_t sg_record_bytes(int32_t n_max) { return sg_record_bytes_ex(n_max, SG_DTYPE_F32); }
 
@@ -442,6 +497,12 @@ int64_t sg_record_bytes_ex(int32_t n_max, int32_t adj_dtype) {
 }
 
 int32_t sg_model_validate(const sg_model_t *model, int64_t *n_params_out, int32_t *path_out) {
+  int64_t wn = 0;
+  if (sg_web_plan_params(model, &wn) == SG_OK && sg_web_lds_ok(model)) {
+    if (n_params_out) *n_params_out = wn;
+    if (path_out) *path_out = 3;
+    return SG_OK;
+  }
   PathChoice c = choose_path(model, true);
   if (c.status != SG_OK) return c.status;
   if (n_params_out) *n_params_out = c.plan.n_params;
@@ -628,6 +689,63 @@ int32_t sg_adam_tf(float *params, float *m, float *v, const float *grad, int64_t
   hipLaunchKernelGGL(sg_adam_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, params, m, v,
                      grad, n, lr, beta1, beta2, eps, weight_decay, beta_powers, reg_loss_out);
   return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
+}
+
+int64_t sg_adam_workspace_bytes(int64_t n) {
+  if (n < 0) return -1;
+  return (int64_t)kAdamBlocks * 8 + 256;
+}
+
+int32_t sg_adam_tf_ex(float *params, float *m, float *v, const float *grad, int64_t n, float lr,
+                      float beta1, float beta2, float eps, float weight_decay, float *beta_powers,
+                      float *reg_loss_out, void *workspace, sg_stream_t stream) {
+  if (!params || !m || !v || !grad || !beta_powers || n <= 0) return SG_ERR_ARG;
+  if (n <= 65536 || !workspace)
+    return sg_adam_tf(params, m, v, grad, n, lr, beta1, beta2, eps, weight_decay, beta_powers,
+                      reg_loss_out, stream);
+  hipStream_t st = (hipStream_t)stream;
+  int64_t nb = (n + 255) / 256;
+  if (nb > kAdamBlocks) nb = kAdamBlocks;
+  double *part = (double *)workspace;
+  hipLaunchKernelGGL(sg_adam_multi, dim3((unsigned)nb), dim3(256), 0, st, params, m, v, grad, n,
+                     lr, beta1, beta2, eps, weight_decay, (const float *)beta_powers, part);
+  hipLaunchKernelGGL(sg_adam_final, dim3(1), dim3(64), 0, st, (const double *)part, (int)nb, beta1,
+                     beta2, weight_decay, beta_powers, reg_loss_out);
+  return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
+}
+
+int64_t sg_web_workspace_bytes(const sg_model_t *model, int64_t chunk) {
+  if (!model || chunk < 0) return -1;
+  return sg_web_ws_bytes(model, chunk);
+}
+
+int32_t sg_web_forward(const sg_model_t *model, const sg_csr_store_t *store,
+                       const int32_t *pair_idx, int64_t n_pairs, int64_t pair_offset,
+                       const float *params, uint64_t seed, float *s_out, void *workspace,
+                       int64_t chunk, sg_stream_t stream) {
+  if (n_pairs < 0 || pair_offset < 0 || chunk < 0) return SG_ERR_ARG;
+  if (n_pairs == 0) return SG_OK;
+  if (!pair_idx || !params || !s_out || !workspace) return SG_ERR_ARG;
+  return sg_web_run(model, store, pair_idx, nullptr, n_pairs, pair_offset, n_pairs, params, seed,
+                    nullptr, 0, s_out, nullptr, nullptr, workspace, chunk, false,
+                    (hipStream_t)stream);
+}
+
+int32_t sg_web_fwd_bwd(const sg_model_t *model, const sg_csr_store_t *store,
+                       const int32_t *pair_idx, const float *labels, int64_t n_pairs,
+                       int64_t pair_offset, int64_t batch_total, const float *params,
+                       uint64_t seed, const float *y_stats, int32_t add_label_term, float *s_out,
+                       float *grad_out, float *loss_out, void *workspace, int64_t chunk,
+                       sg_stream_t stream) {
+  if (n_pairs < 0 || pair_offset < 0 || chunk < 0) return SG_ERR_ARG;
+  if (!params || !grad_out || !workspace) return SG_ERR_ARG;
+  if (n_pairs > 0 && !pair_idx) return SG_ERR_ARG;
+  if (model && model->loss_mode == SG_LOSS_BROADCAST && !y_stats) return SG_ERR_ARG;
+  if (model && model->loss_mode == SG_LOSS_ALIGNED && (batch_total <= 0 || (n_pairs > 0 && !labels)))
+    return SG_ERR_ARG;
+  return sg_web_run(model, store, pair_idx, labels, n_pairs, pair_offset, batch_total, params,
+                    seed, y_stats, add_label_term, s_out, grad_out, loss_out, workspace, chunk,
+                    true, (hipStream_t)stream);
 }
 
 }  // extern "C"

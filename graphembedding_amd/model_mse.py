@@ -73,6 +73,10 @@ class Batch:
     batch_total: int = 0            # global batch size B
     gid_pairs: Optional[np.ndarray] = None
     order: object = None            # torch.int32 [n] processing order (balance()) or None
+    # graph-store path (kernel path 3, config C5): pair ids into a CSR store instead of records
+    csr: object = None              # web.CsrStore
+    pairs: object = None            # torch.int32 [n, 2] store graph ids
+    chunk: int = 0                  # pairs per internal chunk (workspace size)
 
 
 class SiameseGCNTNMSE(object):
@@ -131,6 +135,15 @@ class SiameseGCNTNMSE(object):
         self.seed = int(f.seed)
         self.step_count = 0
         self.grad_hook = None   # e.g. the data-parallel all-reduce (shard.py)
+        self._adam_ws = None
+        if self.n_params > 65536:   # multi-block Adam (config C5: D²K NTN weights)
+            self._adam_ws = torch.empty(_lib.adam_workspace_bytes(self.n_params) // 8 + 1,
+                                        dtype=torch.float64, device=device)
+
+    @property
+    def is_web(self) -> bool:
+        """Graph-store path (sg_web_*, config C5): Padding/NTN width in [32, 512]."""
+        return self.kernel_path == _lib.PATH_WEB
 
     # ---- reference API ------------------------------------------------------
     def apply_final_act_np(self, score):
@@ -140,6 +153,11 @@ class SiameseGCNTNMSE(object):
         """Pre-activation scores of the batch (train.py:87 'test')."""
         torch = self.torch
         s = torch.empty(batch.n_pairs, dtype=torch.float32, device=self.device)
+        if batch.csr is not None:
+            _lib.web_forward(self.sg, batch.csr.to_device(self.device), batch.pairs, batch.n_pairs,
+                             batch.pair_offset, self.params, self._seed(seed), s,
+                             self.web_workspace(batch.chunk), batch.chunk)
+            return s
         _lib.forward(self.sg, batch.records, batch.n_pairs, batch.pair_offset, self.params,
                      self._seed(seed), s, order=batch.order)
         return s
@@ -178,6 +196,8 @@ class SiameseGCNTNMSE(object):
                    batch_total=None) -> Batch:
         """Pack ModelGraph pairs on the host and move them to the device."""
         torch = self.torch
+        if self.is_web:
+            return self.make_web_batch(g1s, g2s, labels, pair_offset, batch_total)
         uniq, index = [], {}
         idx = np.zeros((len(g1s), 2), np.int32)
         for k, (a, b) in enumerate(zip(g1s, g2s)):
@@ -193,6 +213,46 @@ class SiameseGCNTNMSE(object):
         gids = np.array([[a.nxgraph.graph.get('gid', -1), b.nxgraph.graph.get('gid', -1)]
                          for a, b in zip(g1s, g2s)])
         return self.batch_from_records(recs, len(g1s), lab, pair_offset, batch_total, gids)
+
+    def make_web_batch(self, g1s: Sequence, g2s: Sequence, labels=None, pair_offset=0,
+                       batch_total=None, chunk=None) -> Batch:
+        """ModelGraph pairs → a CSR store of the distinct graphs + pair ids (path 3)."""
+        from .web import CsrStore
+        torch = self.torch
+        uniq, index = [], {}
+        idx = np.zeros((len(g1s), 2), np.int32)
+        for k, (a, b) in enumerate(zip(g1s, g2s)):
+            for c, g in enumerate((a, b)):
+                if id(g) not in index:
+                    index[id(g)] = len(uniq)
+                    uniq.append(g)
+                idx[k, c] = index[id(g)]
+        store = CsrStore(uniq, self.input_dim, self.n_max)
+        lab = np.zeros(len(g1s), np.float32) if labels is None else np.asarray(labels, np.float32)
+        gids = np.array([[a.nxgraph.graph.get('gid', -1), b.nxgraph.graph.get('gid', -1)]
+                         for a, b in zip(g1s, g2s)])
+        b = self.web_batch(store, torch.from_numpy(idx).to(self.device), lab, pair_offset,
+                           batch_total, chunk=chunk)
+        b.gid_pairs = gids
+        return b
+
+    def web_batch(self, store, pairs, labels, pair_offset=0, batch_total=None, y_stats=None,
+                  chunk=None) -> Batch:
+        n = int(pairs.shape[0])
+        b = self.batch_from_records(None, n, labels, pair_offset, batch_total, y_stats=y_stats)
+        b.csr, b.pairs = store, pairs
+        b.chunk = int(chunk or min(max(n, 1), 32768))
+        return b
+
+    def web_workspace(self, chunk):
+        torch = self.torch
+        key = ('web', int(chunk))
+        if getattr(self, '_web_ws_key', None) != key:
+            nbytes = _lib.web_workspace_bytes(self.sg, int(chunk))
+            self._web_ws = None
+            self._web_ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device=self.device)
+            self._web_ws_key = key
+        return self._web_ws
 
     def batch_from_records(self, recs, n_pairs, labels, pair_offset=0, batch_total=None,
                            gid_pairs=None, y_stats=None) -> Batch:
@@ -225,6 +285,13 @@ class SiameseGCNTNMSE(object):
     def fwd_bwd(self, batch: Batch, seed=None, s_out=None, add_label_term=True):
         """Forward + loss + backward; leaves Σ∂loss_mse/∂θ in self.grad and the
         shard's loss_mse in self.loss_buf[0]."""
+        if batch.csr is not None:
+            _lib.web_fwd_bwd(self.sg, batch.csr.to_device(self.device), batch.pairs, batch.labels,
+                             batch.n_pairs, batch.pair_offset, batch.batch_total, self.params,
+                             self._seed(seed), batch.y_stats, 1 if add_label_term else 0, s_out,
+                             self.grad, self.loss_buf, self.web_workspace(batch.chunk),
+                             batch.chunk)
+            return
         _lib.fwd_bwd(self.sg, batch.records, batch.n_pairs, batch.pair_offset,
                      batch.batch_total, self.params, self._seed(seed), batch.y_stats,
                      1 if add_label_term else 0, s_out, self.grad, self.loss_buf,
@@ -237,7 +304,7 @@ class SiameseGCNTNMSE(object):
         summation order.  Worth it for batches that are stepped repeatedly
         (all-pairs epochs), not for the reference's B = 5 feeds."""
         torch = self.torch
-        if batch.n_pairs == 0:
+        if batch.n_pairs == 0 or batch.csr is not None:
             return batch
         ws = torch.empty(_lib.pair_order_workspace_bytes(self.sg, batch.n_pairs) // 4 + 1,
                          dtype=torch.int32, device=self.device)
@@ -248,6 +315,11 @@ class SiameseGCNTNMSE(object):
 
     def apply_adam(self):
         f = self.flags
+        if self._adam_ws is not None:
+            _lib.adam_tf_ex(self.params, self.adam_m, self.adam_v, self.grad, f.learning_rate,
+                            self.beta1, self.beta2, self.eps, f.weight_decay, self.beta_powers,
+                            self.reg_buf, self._adam_ws)
+            return
         _lib.adam_tf(self.params, self.adam_m, self.adam_v, self.grad, f.learning_rate,
                      self.beta1, self.beta2, self.eps, f.weight_decay, self.beta_powers,
                      self.reg_buf)

@@ -141,7 +141,8 @@ int32_t sg_version(void);
  * NTN weights_W[D][D][K], weights_V[K][2D], weights_U[K][1], bias[K]).
  * path_out: 1 = fused MFMA path (default stack, n_max = Padding dim <= 12),
  * 2 = fused capacity-32 MFMA path (default stack, n_max = 32, Padding dim in
- * (12, 31]: config C4), 0 = generic path.  Host-only, no GPU.
+ * (12, 31]: config C4), 3 = graph-store path (default stack, Padding dim in
+ * [32, 512]: config C5, sg_web_* entry points), 0 = generic path.  Host-only, no GPU.
  * The capacity-32 path needs sg_workspace_bytes(model, n_pairs) of workspace,
  * which includes 320 B per pair for the NTN weight-gradient operands.
  */
@@ -247,6 +248,58 @@ int32_t sg_sampler_density(int32_t *state, const int32_t *dens_order, const int3
                            int64_t count, int32_t *pairs_out, sg_stream_t stream);
 
 /*
+ * Graph-store path for Web-sized graphs (library 1.5; BASELINE config C5).
+ *
+ * Pair records hold Â densely (n_max² per side), which stops scaling at a few
+ * dozen nodes.  For models that sg_model_validate reports as path 3 (the
+ * default stack GCN(d_in→32, relu) → GCN(32→16) → Dense(16→1, relu) →
+ * Padding(D) → NTN(D, K) with D in [32, 512]) the kernels instead read the
+ * graphs from a device CSR store and a list of pair ids, and the NTN bilinear
+ * term e1ᵀ W[:,:,k] e2 (layers.py:295-298) and its gradients run as batched
+ * MFMA GEMMs over the pairs.  Same math, dropout keys and loss conventions as
+ * sg_forward / sg_fwd_bwd: pair i of the list keys its masks by pair_offset + i.
+ *
+ * sg_csr_store_t is a HOST struct holding DEVICE pointers:
+ *   node_off [n_graphs + 1]  first node of graph g in the node arrays
+ *   types    [n_nodes]       one-hot column of each node (graphs.py:108-111)
+ *   row_ptr  [n_nodes + 1]   CSR row offsets of Â (graphs.py:64-76) into col/val
+ *   col      [nnz]           neighbour as a node index LOCAL to its graph
+ *   val      [nnz]           Â entry (f32 cast of the reference's float64, A11)
+ * Â must be symmetric (undirected graphs, as the reference's).  Every graph
+ * must have 1 <= n <= n_max <= D nodes (tf.pad, quirk A9), checked by the host.
+ */
+typedef struct sg_csr_store {
+  int32_t n_graphs;
+  int32_t n_max;
+  const int32_t *node_off;
+  const int32_t *types;
+  const int32_t *row_ptr;
+  const int32_t *col;
+  const float *val;
+} sg_csr_store_t;
+
+/* Workspace bytes for sg_web_forward / sg_web_fwd_bwd processing chunks of up
+ * to `chunk` pairs (any n_pairs is processed chunk by chunk). */
+int64_t sg_web_workspace_bytes(const sg_model_t *model, int64_t chunk);
+
+/* Pre-activation scores of the pairs pair_idx [n_pairs][2] (store graph ids);
+ * replaces sess.run([pred_sim_without_act()]) like sg_forward. */
+int32_t sg_web_forward(const sg_model_t *model, const sg_csr_store_t *store,
+                       const int32_t *pair_idx, int64_t n_pairs, int64_t pair_offset,
+                       const float *params, uint64_t seed, float *s_out, void *workspace,
+                       int64_t chunk, sg_stream_t stream);
+
+/* Forward + loss + backward over the pairs, as sg_fwd_bwd (same y_stats,
+ * batch_total, add_label_term, grad_out and loss_out conventions).  labels
+ * [n_pairs] are read in aligned loss mode only (may be NULL in broadcast mode). */
+int32_t sg_web_fwd_bwd(const sg_model_t *model, const sg_csr_store_t *store,
+                       const int32_t *pair_idx, const float *labels, int64_t n_pairs,
+                       int64_t pair_offset, int64_t batch_total, const float *params,
+                       uint64_t seed, const float *y_stats, int32_t add_label_term, float *s_out,
+                       float *grad_out, float *loss_out, void *workspace, int64_t chunk,
+                       sg_stream_t stream);
+
+/*
  * TF ApplyAdam (training_ops ApplyAdam, non-Nesterov) with the weight-decay
  * gradient wd·θ added first (models.py:69-73):
  *   g = grad + wd·θ; α = lr·√(1-β2^t)/(1-β1^t); m += (g-m)(1-β1);
@@ -257,6 +310,17 @@ int32_t sg_sampler_density(int32_t *state, const int32_t *dens_order, const int3
 int32_t sg_adam_tf(float *params, float *m, float *v, const float *grad, int64_t n, float lr,
                    float beta1, float beta2, float eps, float weight_decay, float *beta_powers,
                    float *reg_loss_out, sg_stream_t stream);
+
+/*
+ * sg_adam_tf over many blocks (library 1.5), for large parameter vectors (config
+ * C5's NTN has D²K weights): same update and outputs; workspace holds
+ * sg_adam_workspace_bytes(n) bytes of per-block Σθ² partials.  n <= 65536 or a NULL
+ * workspace runs sg_adam_tf.
+ */
+int64_t sg_adam_workspace_bytes(int64_t n);
+int32_t sg_adam_tf_ex(float *params, float *m, float *v, const float *grad, int64_t n, float lr,
+                      float beta1, float beta2, float eps, float weight_decay, float *beta_powers,
+                      float *reg_loss_out, void *workspace, sg_stream_t stream);
 
 #ifdef __cplusplus
 }

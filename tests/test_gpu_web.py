@@ -1,0 +1,117 @@
+"""GPU parity of the graph-store path (kernel path 3, BASELINE config C5: Web-sized
+graphs, Padding / NTN width D in [32, 512]) against the numpy oracle, through the
+C-ABI (sg_web_forward / sg_web_fwd_bwd).  Tolerance 1e-4 as for the record path;
+the oracle's layer math is the same restatement (oracle/siamese_oracle.py) — the
+reference has no Web loader (preprocess_web.py is empty), so the graphs
+are synthetic and the parity anchor is the oracle, not reference fixtures."""
+import numpy as np
+import pytest
+
+from _fixtures import run_oracle_step, small_problem
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+# name: (n_graphs, n_pairs, n_lo, n_hi, D, p_extra, flag overrides)
+CASES = {
+    'd64': (10, 24, 20, 60, 64, {}, 0.15),
+    'd64_nodrop': (10, 24, 20, 60, 64, dict(dropout=0.0), 0.15),
+    'd96_aligned_intended': (10, 20, 30, 90, 96, dict(loss_mode='aligned', ntn_mode='intended'),
+                             0.1),
+    'd64_sigmoid_final': (8, 16, 10, 64, 64, dict(final_act='sigmoid'), 0.15),
+    'd256_sparse': (8, 16, 64, 250, 256, {}, 0.03),
+    'd512_web': (5, 6, 200, 512, 512, {}, 0.012),
+    'd40_single_node': (10, 24, 1, 40, 40, {}, 0.2),
+}
+
+
+def _problem(name, seed=31):
+    G, P, lo, hi, D, ov, pe = CASES[name]
+    return small_problem(n_graphs=G, n_pairs=P, seed=seed, n_lo=lo, n_hi=hi, n_max=D,
+                         flags_overrides=ov, p_extra=pe)
+
+
+def _check_grad(g_gpu, g_ref, tol=TOL):
+    scale = max(1.0, float(np.abs(g_ref).max()))
+    err = float(np.abs(g_gpu - g_ref).max())
+    assert err <= tol * scale, 'max |grad err| {} (scale {})'.format(err, scale)
+
+
+@pytest.mark.parametrize('name', list(CASES))
+def test_web_matches_oracle(gpu, name):
+    prob = _problem(name)
+    model, batch = prob.make_gpu_web_model(device=gpu)
+    seed = 4321
+    s = model.pred_sim_without_act(batch, seed=seed).cpu().numpy()
+    ref = run_oracle_step(prob, seed)
+    np.testing.assert_allclose(s, ref.s, rtol=TOL, atol=TOL)
+    s2 = model.test_scores(batch, seed=seed)
+    model.fwd_bwd(batch, seed=seed)
+    _check_grad(model.grad.cpu().numpy(), ref.grad_mse)
+    loss_mse = float(model.loss_buf[0].item())
+    assert abs(loss_mse - ref.loss_mse) <= TOL * max(1.0, abs(ref.loss_mse))
+    model.apply_adam()
+    reg = float(model.reg_buf[0].item())
+    assert abs(loss_mse + reg - ref.loss) <= TOL * max(1.0, abs(ref.loss))
+    np.testing.assert_allclose(model.params.cpu().numpy(), ref.new_params, rtol=0, atol=2e-5)
+    assert np.array_equal(s2.astype(np.float32), s)
+
+
+def test_web_padding_value(gpu):
+    """Non-zero padding_value: the NTN input is non-zero past the graph's nodes, so
+    the kernels run the full D extent."""
+    ov = dict(layer_3='Padding:max_in_dims=64,padding_value=1',
+              layer_4='NTN:input_dim=64,feature_map_dim=10,inneract=relu,dropout=True,bias=True')
+    prob = small_problem(n_graphs=8, n_pairs=12, seed=9, n_lo=10, n_hi=50, n_max=64,
+                         flags_overrides=ov)
+    model, batch = prob.make_gpu_web_model(device=gpu)
+    ref = run_oracle_step(prob, 77)
+    np.testing.assert_allclose(model.pred_sim_without_act(batch, seed=77).cpu().numpy(), ref.s,
+                               rtol=TOL, atol=TOL)
+    model.fwd_bwd(batch, seed=77)
+    _check_grad(model.grad.cpu().numpy(), ref.grad_mse)
+
+
+def test_web_chunks_shards_determinism(gpu):
+    """Chunked == one chunk (scores bitwise, gradient to fp32 order), sharded forward
+    == unsharded, fwd_bwd bitwise reproducible, gradient additive over shards."""
+    import torch
+    prob = small_problem(n_graphs=24, n_pairs=700, seed=12, n_lo=20, n_hi=128, n_max=128,
+                         p_extra=0.05)
+    model, full = prob.make_gpu_web_model(device=gpu)
+    _, chunked = prob.make_gpu_web_model(device=gpu, chunk=97)
+    seed = 5
+    s_full = model.pred_sim_without_act(full, seed=seed).cpu().numpy()
+    s_ch = model.pred_sim_without_act(chunked, seed=seed).cpu().numpy()
+    assert np.array_equal(s_full, s_ch)
+    model.fwd_bwd(full, seed=seed)
+    g_full, l_full = model.grad.clone(), float(model.loss_buf[0].item())
+    model.fwd_bwd(full, seed=seed)
+    assert torch.equal(g_full, model.grad), 'sg_web_fwd_bwd is not bitwise reproducible'
+    model.fwd_bwd(chunked, seed=seed)
+    g = model.grad.cpu().numpy()
+    _check_grad(g, g_full.cpu().numpy(), tol=1e-5)
+    # shards of the pair list keyed by their global offset
+    h = full.n_pairs // 2
+    b0 = model.web_batch(full.csr, full.pairs[:h], full.labels[:h], 0, full.n_pairs,
+                         y_stats=full.y_stats)
+    b1 = model.web_batch(full.csr, full.pairs[h:], full.labels[h:], h, full.n_pairs,
+                         y_stats=full.y_stats)
+    s0 = model.pred_sim_without_act(b0, seed=seed).cpu().numpy()
+    s1 = model.pred_sim_without_act(b1, seed=seed).cpu().numpy()
+    assert np.array_equal(np.concatenate([s0, s1]), s_full)
+    model.fwd_bwd(b0, seed=seed, add_label_term=True)
+    g0, l0 = model.grad.clone(), float(model.loss_buf[0].item())
+    model.fwd_bwd(b1, seed=seed, add_label_term=False)
+    _check_grad((g0 + model.grad).cpu().numpy(), g_full.cpu().numpy(), tol=1e-5)
+    assert abs(l0 + float(model.loss_buf[0].item()) - l_full) <= 1e-5 * max(1.0, abs(l_full))
+
+
+def test_web_empty_batch(gpu):
+    prob = _problem('d64')
+    model, batch = prob.make_gpu_web_model(device=gpu)
+    empty = model.web_batch(batch.csr, batch.pairs[:0], batch.labels[:0], 0, 1,
+                            y_stats=batch.y_stats)
+    model.fwd_bwd(empty, seed=1)
+    assert float(model.grad.abs().max().item()) == 0.0
