@@ -2,7 +2,10 @@
 
 (--dataset syn_aids10knef: config C4, AIDS10knef-shaped all-pairs, 100.4 M pairs per
 step, Padding/NTN 30 on the capacity-32 fused kernel; records resident when a rank's
-shard fits HBM, else packed chunk by chunk inside the step.)
+shard fits HBM, else packed chunk by chunk inside the step.
+ --dataset syn_web: config C5, 1,100 Web-sized synthetic graphs (N ~ U{64..512}),
+1.21 M all-pairs per step, Padding/NTN 512 on the graph-store path: CSR store + pair
+ids, NTN as MFMA GEMMs over the pairs.)
 
 One step = one pass of the hot path over the whole 700² = 490,000-pair
 all-pairs batch: fused forward + broadcast-MSE loss + backward over this rank's
@@ -31,8 +34,10 @@ FP32_PEAK_TFLOPS = 157.3       # gfx950 fp32 peak (vector = f32 MFMA), MI355X_MI
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
-    p.add_argument('--steps', type=int, default=50)
-    p.add_argument('--warmup', type=int, default=10)
+    p.add_argument('--steps', type=int, default=None, help='default 50 (C5: 3)')
+    p.add_argument('--warmup', type=int, default=None, help='default 10 (C5: 1)')
+    p.add_argument('--web-chunk', type=int, default=65536,
+                   help='C5: pairs per internal chunk of sg_web_fwd_bwd')
     p.add_argument('--dataset', default='syn_aids700nef')
     p.add_argument('--dropout', type=float, default=0.1)
     p.add_argument('--records', choices=('f32', 'bf16'), default='f32',
@@ -72,6 +77,11 @@ def cpu_baseline(gs, labels, flags, n_sample, D=None):
 
 def main():
     args = parse()
+    web = args.dataset == 'syn_web'
+    if args.steps is None:
+        args.steps = 3 if web else 50
+    if args.warmup is None:
+        args.warmup = 1 if web else 10
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -91,14 +101,19 @@ def main():
     from graphembedding_amd.shard import make_allreduce_hook
 
     c4 = args.dataset == 'syn_aids10knef'
-    D = 30 if c4 else 10
+    D = 512 if web else (30 if c4 else 10)
     fl = dict(dropout=args.dropout, record_dtype=args.records)
     if c4:   # AIDS10k: N <= 30 needs Padding / NTN input_dim 30
         fl.update(layer_3='Padding:max_in_dims=30,padding_value=0',
                   layer_4='NTN:input_dim=30,feature_map_dim=10,inneract=relu,dropout=True,'
                           'bias=True')
+    if web:   # Web: N <= 512 needs Padding / NTN input_dim 512
+        fl.update(layer_3='Padding:max_in_dims=512,padding_value=0',
+                  layer_4='NTN:input_dim=512,feature_map_dim=10,inneract=relu,dropout=True,'
+                          'bias=True')
     flags = Flags(**fl)
-    gs = load_graph_set(args.dataset, n_max=32 if c4 else 10)
+    gs = load_graph_set(args.dataset, n_max=512 if web else (32 if c4 else 10),
+                        with_store=not web)
     labels = gs.label_matrix(flags.yeta)
     model = SiameseGCNTNMSE(gs.d_in, flags, device=device, n_max=gs.n_max)
     assert model.n_max == gs.n_max
@@ -106,7 +121,11 @@ def main():
     srank, sworld = (0, ew) if ew else (rank, world)
     balance = args.order == 'class'
     streamed = False
-    if c4:
+    if web:
+        from graphembedding_amd.web import WebAllPairs
+        shard = WebAllPairs(gs, labels, srank, sworld, device=device, chunk=args.web_chunk)
+        batch = shard.batch(model)
+    elif c4:
         from graphembedding_amd.shard import shard_range
         a, b = shard_range(len(gs.graphs) ** 2, srank, sworld)
         from graphembedding_amd.packer import record_words
@@ -115,11 +134,12 @@ def main():
         shard = AllPairsStream(gs, labels, srank, sworld, device=device, chunk=args.chunk,
                                dtype=args.records, balance=balance)
         batch = None
-    else:
+    if not web and not streamed:
         shard = AllPairsShard(gs, labels, srank, sworld, device=device, dtype=args.records)
         batch = shard.batch(model, balance=balance)
     hook = make_allreduce_hook() if world > 1 else None
-    model.workspace(shard.chunk if streamed else batch.n_pairs)
+    if not web:
+        model.workspace(shard.chunk if streamed else batch.n_pairs)
     stream = torch.cuda.current_stream()
 
     ev = []
@@ -168,8 +188,8 @@ def main():
     loss = float(model.loss_buf[0].item() + model.reg_buf[0].item())
 
     if rank == 0:
-        flops_pair = gs.flops_per_pair(D=D)
-        bytes_pair = shard.record_bytes
+        flops_pair = gs.flops_per_pair_web() if web else gs.flops_per_pair(D=D)
+        bytes_pair = gs.csr_bytes_per_pair() if web else shard.record_bytes
         kern_pairs_s = shard.n / (kern_ms * 1e-3)
         achieved_tf = kern_pairs_s * flops_pair / 1e12
         achieved_gbs = kern_pairs_s * bytes_pair / 1e9
@@ -184,13 +204,33 @@ def main():
         cpu = None
         if world == 1 and args.cpu_sample >= 0:
             try:
-                cpu = cpu_baseline(gs, labels, flags, args.cpu_sample, D=D)
+                if web:
+                    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+                    from oracle import cpu_ref
+                    gsd = gs
+                    cpu = cpu_ref.time_web_sample(gsd, labels, flags, n_sample=64,
+                                                  target_s=12.0)
+                else:
+                    cpu = cpu_baseline(gs, labels, flags, args.cpu_sample, D=D)
             except Exception as e:  # reported, never fatal for the GPU number
                 cpu = {'value': None, 'unit': 'graph-pairs/s', 'cores': 0, 'kind': 'port',
                        'sample': 'failed: {}'.format(e)}
+        name = 'Web' if web else ('AIDS10knef' if c4 else 'AIDS700')
+        if web:
+            workload = ('Web-sized all-pairs ({} synthetic graphs, N ~ U{{64..512}}, {:,} ordered '
+                        'pairs), Padding/NTN 512'.format(len(gs.graphs), total_pairs))
+            inputs = ('CSR graph store + size-ordered pair ids resident in HBM, {} pairs per '
+                      'internal chunk'.format(shard.chunk))
+            records = 'CSR store (no pair records), {:.0f} B/pair of graph input'.format(bytes_pair)
+        else:
+            workload = ('AIDS10knef all-pairs (10,018 graphs, N <= 30, {:,} ordered '
+                        'pairs), Padding/NTN 30' if c4 else
+                        'AIDS700nef all-pairs (700 graphs, {:,} ordered pairs)').format(total_pairs)
+            inputs = ('packed in chunks of {} pairs inside the step'.format(shard.chunk)
+                      if streamed else 'records resident in HBM')
+            records = '{} Â, {} B/pair'.format(args.records, bytes_pair)
         out = {
-            'metric': 'graph-pairs/sec (Siamese fwd+bwd), {} all-pairs'.format(
-                'AIDS10knef' if c4 else 'AIDS700'),
+            'metric': 'graph-pairs/sec (Siamese fwd+bwd), {} all-pairs'.format(name),
             'value': value,
             'unit': 'graph-pairs/s',
             'n_gpus': world,
@@ -202,25 +242,24 @@ def main():
             'vs_baseline': None,
             'dtype': 'f32',
             'data': 'synthetic ({}-shaped graphs + GED labels, BASELINE.md §3)'.format(
-                'AIDS10knef' if c4 else 'AIDS700nef'),
-            'config': {'workload': ('AIDS10knef all-pairs (10,018 graphs, N <= 30, {:,} ordered '
-                                    'pairs), Padding/NTN 30' if c4 else
-                                    'AIDS700nef all-pairs (700 graphs, {:,} ordered pairs)'
-                                    ).format(total_pairs) +
+                'Web' if web else ('AIDS10knef' if c4 else 'AIDS700nef')),
+            'config': {'workload': workload +
                                    ', default 5-layer Siamese GCN-NTN, dropout {}'.format(args.dropout),
                        'global_batch': total_pairs, 'n_max': gs.n_max, 'd_in': gs.d_in,
                        'kernel_path': _lib.PATH_NAMES[model.kernel_path],
-                       'records': '{} Â, {} B/pair'.format(args.records, bytes_pair),
-                       'order': args.order,
-                       'inputs': ('packed in chunks of {} pairs inside the step'.format(shard.chunk)
-                                  if streamed else 'records resident in HBM'),
+                       'records': records,
+                       'order': 'size buckets' if web else args.order,
+                       'inputs': inputs,
                        'parallelism': 'dp{}'.format(world)},
             'roofline': {'bound': 'mfma', 'achieved': achieved_tf, 'peak': FP32_PEAK_TFLOPS,
                          'unit': 'TFLOP/s', 'frac': achieved_tf / FP32_PEAK_TFLOPS,
                          'traffic': traffic,
                          'note': 'fp32 compute roof (gfx950 vector fp32 == f32 MFMA peak); '
-                                 'algorithmic {:.0f} FLOP/pair x {} pairs per launch / sg_fwd_bwd '
-                                 'event time {:.3f} ms'.format(flops_pair, shard.n, kern_ms)},
+                                 'algorithmic {:.0f} FLOP/pair x {} pairs per launch / {} '
+                                 'event time {:.3f} ms'.format(
+                                     flops_pair, shard.n,
+                                     'sg_web_fwd_bwd (all its kernels)' if web else 'sg_fwd_bwd',
+                                     kern_ms)},
             'roofline_hbm': {'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                              'frac': achieved_gbs / HBM_PEAK_GBS,
                              'bytes_per_pair': bytes_pair},

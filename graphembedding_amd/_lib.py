@@ -47,7 +47,8 @@ class SgCsrStore(ctypes.Structure):
     """sg_csr_store_t: host struct of device pointers (graph-store path, config C5)."""
     _fields_ = [('n_graphs', ctypes.c_int32), ('n_max', ctypes.c_int32),
                 ('node_off', ctypes.c_void_p), ('types', ctypes.c_void_p),
-                ('row_ptr', ctypes.c_void_p), ('col', ctypes.c_void_p), ('val', ctypes.c_void_p)]
+                ('row_ptr', ctypes.c_void_p), ('col', ctypes.c_void_p), ('val', ctypes.c_void_p),
+                ('max_nnz', ctypes.c_int32)]
 
 
 class SiameseHipError(RuntimeError):
@@ -322,8 +323,9 @@ def adam_workspace_bytes(n: int) -> int:
     return int(lib().sg_adam_workspace_bytes(int(n)))
 
 
-def csr_struct(n_graphs, n_max, node_off, types, row_ptr, col, val) -> SgCsrStore:
+def csr_struct(n_graphs, n_max, node_off, types, row_ptr, col, val, max_nnz=0) -> SgCsrStore:
     s = SgCsrStore()
+    s.max_nnz = int(max_nnz)
     s.n_graphs = int(n_graphs)
     s.n_max = int(n_max)
     s.node_off, s.types, s.row_ptr = _ptr(node_off), _ptr(types), _ptr(row_ptr)

@@ -37,6 +37,28 @@ class GraphSet:
         d = d.astype(np.float32).astype(np.float64)           # float32 placeholder feed
         return np.exp(-yeta * d * d).astype(np.float32)
 
+    def flops_per_pair_web(self, h1=32, h2=16, K=10) -> float:
+        """Config C5: SURVEY §8(d) per-graph GCN/Dense terms, and the NTN terms on the
+        pair's nonzero structure (x is zero beyond each graph's nodes, so the
+        bilinear term is n1·n2 per k instead of D²): fwd K(2 n1 n2 + 2(n1+n2)),
+        bwd twice that.  Averaged over the all-pairs stream."""
+        n = np.array([g.number_of_nodes() for g in self.graphs], dtype=np.float64)
+        e = np.array([g.number_of_edges() for g in self.graphs], dtype=np.float64)
+        nnz = n + 2 * e
+        fwd = 2 * h1 * n + 2 * h1 * nnz + 2 * n * h1 * h2 + 2 * h2 * nnz + 2 * n * h2
+        bwd = (2 * h1 * nnz + 2 * h1 * n) + (2 * h2 * nnz + 4 * n * h1 * h2) + 4 * n * h2
+        nm = n.mean()
+        ntn_f = K * (2 * (n[:, None] * n[None, :]).mean() + 2 * 2 * nm)
+        return float(2 * (fwd + bwd).mean() + 3 * ntn_f)
+
+    def csr_bytes_per_pair(self) -> float:
+        """Algorithmic input bytes of a pair on the graph-store path: both graphs'
+        CSR rows (row_ptr + col + val) and types, plus the pair ids and label."""
+        n = np.array([g.number_of_nodes() for g in self.graphs], dtype=np.float64)
+        e = np.array([g.number_of_edges() for g in self.graphs], dtype=np.float64)
+        per_graph = 4 * (n + 1) + 4 * n + 8 * (n + 2 * e)
+        return float(2 * per_graph.mean() + 12)
+
     def flops_per_pair(self, h1=32, h2=16, D=10, K=10) -> float:
         """Algorithmic FLOPs per pair, fwd+bwd (SURVEY §8(d) formula), averaged
         over the all-pairs stream (every graph is g1 G times and g2 G times)."""
@@ -49,13 +71,15 @@ class GraphSet:
         return float(2 * (fwd + bwd).mean() + 3 * ntn_f)
 
 
-def load_graph_set(name: str = 'syn_aids700nef', n_max: int = 10, seed: int = 123) -> GraphSet:
+def load_graph_set(name: str = 'syn_aids700nef', n_max: int = 10, seed: int = 123,
+                   with_store: bool = True) -> GraphSet:
     tr, te = synthetic_graphs(name, seed)
     graphs = tr + te
     # sorted (not set-order) columns: identical encoding on every rank (quirk A7)
     enc = NodeFeatureOneHotEncoder(graphs, 'type').pin_sorted()
     mgs = [ModelGraph(g, enc) for g in graphs]
-    store = GraphStore(mgs, n_max, enc.input_dim())
+    # dense-slot store for the record paths; the graph-store path (web.py) builds CSR
+    store = GraphStore(mgs, n_max, enc.input_dim()) if with_store else None
     return GraphSet(graphs=graphs, mgs=mgs, d_in=enc.input_dim(), n_max=n_max, store=store,
                     ged=synthetic_ged_matrix(graphs))
 

@@ -42,7 +42,6 @@ using sgk::mfma4;
 constexpr int WH1 = 32, WH2 = 16;   // GCN widths of the default stack
 constexpr int WKP = 16;             // NTN K capacity (gm rows, head slab)
 constexpr int WMAXD = 512;          // max Padding / NTN width (LDS budget of one instance)
-constexpr int GW = 8;               // waves per instance workgroup
 constexpr int TB = 128;             // GEMM tile edge
 constexpr int MKS = 20;             // MK LDS tile row stride (16 + 4): conflict-free b128 reads
 constexpr int KMS = TB + 4;         // KM LDS tile row stride
@@ -237,7 +236,15 @@ __global__ void __launch_bounds__(256) web_wprep_h(const float *__restrict__ Wg,
 
 // ---------------------------------------------------------------------------
 // Per-instance GCN → Dense → Padding stack (+ backward with recompute).
+// One workgroup per instance (pair, side); node tiles of 16 rows, tile t on wave
+// t % waves (N <= 512: 32 tiles).  The instance's CSR rows
+// are staged in LDS when they fit (one coalesced copy, then ~100-cycle reads in
+// the sparse loops instead of a dependent global-load chain per neighbour).
 // ---------------------------------------------------------------------------
+// waves per instance workgroup: 16 forward (2 tiles per wave), 8 backward (4 tiles
+// per wave: the backward needs more than the 128 VGPRs of a 16-wave block)
+__host__ __device__ constexpr int gcn_gw(bool bwd) { return bwd ? 8 : 16; }
+
 struct GcnArgs {
   const int32_t *node_off, *types, *row_ptr, *col;
   const float *val;
@@ -249,20 +256,23 @@ struct GcnArgs {
   float *slab;       // [gridDim.x][n_gcn] (backward, accumulated)
   uint32_t key, thr0, thr1, thr2, thr4;
   float ik0, ik1, ik2, ik4, padv;
-  int d_in, D, Dp, n_gcn, n_max;
+  int d_in, D, Dp, n_gcn, n_max, max_nnz;
   int ob0, oW1, ob1, oWd, obd;
 };
 
-// LDS (floats): tables, then the instance region sized for n_max nodes
+// LDS (4-byte words): tables, then the instance region sized for n_max nodes
 //   sW0 [(d_in+1)][32] = W0·ik0 (row d_in zero: dropped one-hot rows), sb0 [32],
 //   sW1 [32][16] = W1·ik1, sW1T [16][32] = (W1·ik1)ᵀ, sb1 [16], sWd [16] = Wd·ik2
-//   sEt [N16] effective type (d_in when dropped / absent), sZ1 [N16][16],
-//   sD1 [N16][32] (backward: D1' = H1·m1, later gP0), sG1 [N16][16] (backward: gZ1)
+//   sEt [N16] effective type (d_in when dropped / absent),
+//   sZ1 [N16][16]: Z1, then (backward) gZ1,
+//   sD1 [N16][32] (backward): D1' = H1·m1, then gP0,
+//   sScr [8 waves][16][16] (backward): a wave's gS1 tile, re-read as MFMA B operand,
+//   CSR (LCSR): row offsets [N16 + 1], columns [max_nnz], values [max_nnz].
 struct GcnLds {
-  int w0, b0, w1, w1t, b1, wd, tables, et, z1, d1, g1, total;
+  int w0, b0, w1, w1t, b1, wd, tables, et, z1, d1, scr, rp, col, val, total;
 };
 
-__host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, bool bwd) {
+__host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, int max_nnz, bool bwd, bool lcsr) {
   GcnLds L;
   int o = 0;
   L.w0 = o; o += (d_in + 1) * WH1;
@@ -276,27 +286,48 @@ __host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, bool bwd) {
   L.et = o; o += n16;
   L.z1 = o; o += n16 * WH2;
   L.d1 = o; if (bwd) o += n16 * WH1;
-  L.g1 = o; if (bwd) o += n16 * WH2;
+  L.scr = o; if (bwd) o += gcn_gw(true) * 256;
+  L.rp = o; if (lcsr) o += (n16 + 4) & ~3;
+  L.col = o; if (lcsr) o += (max_nnz + 3) & ~3;
+  L.val = o; if (lcsr) o += (max_nnz + 3) & ~3;
   L.total = o;
   return L;
 }
 
-template <bool BWD, int NTB>
-__global__ void __launch_bounds__(64 * GW) web_gcn_kernel(GcnArgs A) {
+// Σ_e val[e] · f(col[e]) over one CSR row, four neighbours' loads in flight at a time
+template <typename F>
+__device__ __forceinline__ void csr_row(const int *__restrict__ col, const float *__restrict__ val,
+                                        int e0, int e1, F f) {
+  int e = e0;
+  for (; e + 4 <= e1; e += 4) {
+    const int c0 = col[e], c1 = col[e + 1], c2 = col[e + 2], c3 = col[e + 3];
+    const float v0 = val[e], v1 = val[e + 1], v2 = val[e + 2], v3 = val[e + 3];
+    f(c0, v0);
+    f(c1, v1);
+    f(c2, v2);
+    f(c3, v3);
+  }
+  for (; e < e1; ++e) f(col[e], val[e]);
+}
+
+template <bool BWD, int NTB, bool LCSR>
+__global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
+  constexpr int GW_ = gcn_gw(BWD), NT = 64 * GW_, GCN_TPW = 32 / GW_;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   const int i = l & 15, g = l >> 4;
   const int d_in = A.d_in;
   const int n16max = (A.n_max + 15) & ~15;
-  const GcnLds L = gcn_lds(d_in, n16max, BWD);
+  const GcnLds L = gcn_lds(d_in, n16max, A.max_nnz, BWD, LCSR);
   float *sW0 = sm + L.w0, *sb0 = sm + L.b0, *sW1 = sm + L.w1, *sW1T = sm + L.w1t;
   float *sb1 = sm + L.b1, *sWd = sm + L.wd;
   int *sEt = (int *)(sm + L.et);
-  float *sZ1 = sm + L.z1, *sD1 = sm + L.d1, *sG1 = sm + L.g1;
+  float *sZ1 = sm + L.z1, *sD1 = sm + L.d1, *scr = sm + L.scr + w * 256;
+  int *sRp = (int *)(sm + L.rp), *sCol = (int *)(sm + L.col);
+  float *sVal = sm + L.val;
   const float *prm = A.params;
-  for (int x = tid; x < (d_in + 1) * WH1; x += 64 * GW)
-    sW0[x] = x < d_in * WH1 ? prm[x] * A.ik0 : 0.f;
-  for (int x = tid; x < WH1 * WH2; x += 64 * GW) {
+  for (int x = tid; x < (d_in + 1) * WH1; x += NT) sW0[x] = x < d_in * WH1 ? prm[x] * A.ik0 : 0.f;
+  for (int x = tid; x < WH1 * WH2; x += NT) {
     const float v = prm[A.oW1 + x] * A.ik1;
     sW1[x] = v;
     sW1T[(x % WH2) * WH1 + x / WH2] = v;
@@ -315,10 +346,10 @@ __global__ void __launch_bounds__(64 * GW) web_gcn_kernel(GcnArgs A) {
 #pragma unroll
   for (int t = 0; t < NTB; ++t) aW0[t][0] = aW0[t][1] = f4{0.f, 0.f, 0.f, 0.f};
   aW1[0] = aW1[1] = f4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();
 
   const int64_t n_inst = 2 * A.n_pairs;
   for (int64_t q = blockIdx.x; q < n_inst; q += gridDim.x) {
+    __syncthreads();   // the previous instance (or the table build) is done with the LDS
     const int64_t p = q >> 1;
     const int side = (int)(q & 1);
     const int gid = A.pairs[2 * p + side];
@@ -327,14 +358,30 @@ __global__ void __launch_bounds__(64 * GW) web_gcn_kernel(GcnArgs A) {
     const int n16 = (N + 15) & ~15;
     const int ntile = n16 >> 4;
     const uint32_t pk = sg_pair_key(A.key, (uint32_t)(A.pair_offset + p));
-    const int *__restrict__ rp = A.row_ptr + o;
+    const int *rp;
+    const int *cl;
+    const float *vl;
+    if (LCSR) {
+      const int eb = A.row_ptr[o], nnz = A.row_ptr[o + N] - eb;
+      for (int n = tid; n <= N; n += NT) sRp[n] = A.row_ptr[o + n] - eb;
+      for (int e = tid; e < nnz; e += NT) {
+        sCol[e] = A.col[eb + e];
+        sVal[e] = A.val[eb + e];
+      }
+      rp = sRp; cl = sCol; vl = sVal;
+    } else {
+      rp = A.row_ptr + o; cl = A.col; vl = A.val;
+    }
     // effective one-hot column per node (sparse dropout of X, layer 0, e = node)
-    for (int n = tid; n < n16; n += 64 * GW)
+    for (int n = tid; n < n16; n += NT)
       sEt[n] = (n < N && sg_keep(pk, 0, side, n, A.thr0)) ? A.types[o + n] : d_in;
     __syncthreads();
 
     // ---- forward: H1 (lane (i, g): node 16t+i, features 16c + 4g + s), D1', Z1 ----
-    for (int t = w; t < ntile; t += GW) {
+#pragma unroll
+    for (int u = 0; u < GCN_TPW; ++u) {
+      const int t = w + u * GW_;
+      if (t >= ntile) break;
       const int n = 16 * t + i;
       float h[8];
 #pragma unroll
@@ -343,17 +390,14 @@ __global__ void __launch_bounds__(64 * GW) web_gcn_kernel(GcnArgs A) {
         h[4 * c] = b.x; h[4 * c + 1] = b.y; h[4 * c + 2] = b.z; h[4 * c + 3] = b.w;
       }
       if (n < N) {
-        const int e0 = rp[n], e1 = rp[n + 1];
-        for (int e = e0; e < e1; ++e) {
-          const int mm = A.col[e];
-          const float v = A.val[e];
+        csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
           const float *wr = sW0 + sEt[mm] * WH1 + 4 * g;
           const float4 wa = *(const float4 *)wr, wb = *(const float4 *)(wr + 16);
           h[0] = fmaf(v, wa.x, h[0]); h[1] = fmaf(v, wa.y, h[1]);
           h[2] = fmaf(v, wa.z, h[2]); h[3] = fmaf(v, wa.w, h[3]);
           h[4] = fmaf(v, wb.x, h[4]); h[5] = fmaf(v, wb.y, h[5]);
           h[6] = fmaf(v, wb.z, h[6]); h[7] = fmaf(v, wb.w, h[7]);
-        }
+        });
 #pragma unroll
         for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -381,20 +425,21 @@ __global__ void __launch_bounds__(64 * GW) web_gcn_kernel(GcnArgs A) {
     __syncthreads();
 
     // ---- H2 (lane (i, g): node 16t+i, features 4g..4g+3), Dense, Padding, NTN input ----
-    for (int t = w; t < ntile; t += GW) {
+    float gzr[GCN_TPW][4];
+#pragma unroll
+    for (int u = 0; u < GCN_TPW; ++u) {
+      const int t = w + u * GW_;
+      if (t >= ntile) break;
       const int n = 16 * t + i;
       float h2[4] = {0.f, 0.f, 0.f, 0.f};
       if (n < N) {
         const float4 b = *(const float4 *)(sb1 + 4 * g);
         h2[0] = b.x; h2[1] = b.y; h2[2] = b.z; h2[3] = b.w;
-        const int e0 = rp[n], e1 = rp[n + 1];
-        for (int e = e0; e < e1; ++e) {
-          const int mm = A.col[e];
-          const float v = A.val[e];
+        csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
           const float4 zz = *(const float4 *)(sZ1 + mm * WH2 + 4 * g);
           h2[0] = fmaf(v, zz.x, h2[0]); h2[1] = fmaf(v, zz.y, h2[1]);
           h2[2] = fmaf(v, zz.z, h2[2]); h2[3] = fmaf(v, zz.w, h2[3]);
-        }
+        });
       }
       bool k2[4];
       float part = 0.f;
@@ -410,58 +455,62 @@ __global__ void __launch_bounds__(64 * GW) web_gcn_kernel(GcnArgs A) {
         if (g == 0 && n < N)
           A.X[((int64_t)side * A.Cp + p) * A.Dp + n] = k4 ? z * A.ik4 : 0.f;
       } else {
-        // Dense / Padding / NTN-input backward; gZ1 of this node into sG1
+        // Dense / Padding / NTN-input backward: gZ1 (= gH2, identity act) in registers
         const float gx = k4 ? A.GX[((int64_t)side * A.Cp + p) * A.Dp + n] * A.ik4 : 0.f;
         const float gp = (n < N && pre > 0.f) ? gx : 0.f;
         if (g == 0) aBd += gp;
-        float gz[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           aWd[s] = fmaf(k2[s] ? h2[s] : 0.f, gp, aWd[s]);
-          gz[s] = k2[s] ? gp * sWd[4 * g + s] : 0.f;   // gH2 = gZ1 (identity act)
-          aB1[s] += gz[s];
+          gzr[u][s] = k2[s] ? gp * sWd[4 * g + s] : 0.f;
+          aB1[s] += gzr[u][s];
         }
-        *(float4 *)(sG1 + n * WH2 + 4 * g) = make_float4(gz[0], gz[1], gz[2], gz[3]);
       }
     }
     if (!BWD) {
       // Padding rows [N, Dp): padding_value (zero beyond D), after the NTN-input dropout
-      for (int a = N + tid; a < A.Dp; a += 64 * GW)
+      for (int a = N + tid; a < A.Dp; a += NT)
         A.X[((int64_t)side * A.Cp + p) * A.Dp + a] =
             (a < A.D && A.padv != 0.f && sg_keep(pk, 4, side, (uint32_t)a, A.thr4))
                 ? A.padv * A.ik4 : 0.f;
-      __syncthreads();   // sEt / sZ1 are rewritten by the next instance
       continue;
+    }
+    __syncthreads();   // every wave is done reading Z1: it becomes gZ1
+#pragma unroll
+    for (int u = 0; u < GCN_TPW; ++u) {
+      const int t = w + u * GW_;
+      if (t >= ntile) break;
+      *(float4 *)(sZ1 + (16 * t + i) * WH2 + 4 * g) =
+          make_float4(gzr[u][0], gzr[u][1], gzr[u][2], gzr[u][3]);
     }
     __syncthreads();
 
     // ---- gS1 = Â·gZ1 (lane (i, g): node 16t+i, j = 4g..4g+3); gD1 = gS1·W1ᵀ; gW1 ----
-    for (int t = w; t < ntile; t += GW) {
+#pragma unroll
+    for (int u = 0; u < GCN_TPW; ++u) {
+      const int t = w + u * GW_;
+      if (t >= ntile) break;
       const int n = 16 * t + i;
       float q4[4] = {0.f, 0.f, 0.f, 0.f};
-      if (n < N) {
-        const int e0 = rp[n], e1 = rp[n + 1];
-        for (int e = e0; e < e1; ++e) {
-          const int mm = A.col[e];
-          const float v = A.val[e];
-          const float4 gg = *(const float4 *)(sG1 + mm * WH2 + 4 * g);
+      if (n < N)
+        csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
+          const float4 gg = *(const float4 *)(sZ1 + mm * WH2 + 4 * g);
           q4[0] = fmaf(v, gg.x, q4[0]); q4[1] = fmaf(v, gg.y, q4[1]);
           q4[2] = fmaf(v, gg.z, q4[2]); q4[3] = fmaf(v, gg.w, q4[3]);
-        }
-      }
+        });
       // gD1·ik1 (rows n = 16t + 4g + r, column f = 16cb + i)
       f4 gd[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
         for (int s = 0; s < 4; ++s) gd[cb] = mfma4(q4[s], sW1T[(4 * g + s) * WH1 + 16 * cb + i], gd[cb]);
-      // gS1 of this tile into sZ1 (dead: every wave passed the H2 loop), read back as B
-      *(float4 *)(sZ1 + n * WH2 + 4 * g) = make_float4(q4[0], q4[1], q4[2], q4[3]);
+      // the tile's gS1 through the wave's scratch, read back as the B operand of gW1
+      *(float4 *)(scr + i * WH2 + 4 * g) = make_float4(q4[0], q4[1], q4[2], q4[3]);
       sg_wsync();
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int nn = 16 * t + 4 * g + s;
-        const float b = sZ1[nn * WH2 + i];
+        const float b = scr[(4 * g + s) * WH2 + i];
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) aW1[cb] = mfma4(sD1[nn * WH1 + 16 * cb + i], b, aW1[cb]);
       }
@@ -480,7 +529,10 @@ __global__ void __launch_bounds__(64 * GW) web_gcn_kernel(GcnArgs A) {
     __syncthreads();
 
     // ---- gS0 = Â·gP0 (rows n = 16t + 4g + s, features i, 16 + i); gW0 += Xᵀ·(scale0·gS0) ----
-    for (int t = w; t < ntile; t += GW) {
+#pragma unroll
+    for (int u = 0; u < GCN_TPW; ++u) {
+      const int t = w + u * GW_;
+      if (t >= ntile) break;
       float bq[4][2];
       int et[4];
 #pragma unroll
@@ -488,15 +540,11 @@ __global__ void __launch_bounds__(64 * GW) web_gcn_kernel(GcnArgs A) {
         const int n = 16 * t + 4 * g + s;
         float q0 = 0.f, q1 = 0.f;
         et[s] = sEt[n];
-        if (n < N && et[s] < d_in) {
-          const int e0 = rp[n], e1 = rp[n + 1];
-          for (int e = e0; e < e1; ++e) {
-            const int mm = A.col[e];
-            const float v = A.val[e];
+        if (n < N && et[s] < d_in)
+          csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
             q0 = fmaf(v, sD1[mm * WH1 + i], q0);
             q1 = fmaf(v, sD1[mm * WH1 + 16 + i], q1);
-          }
-        }
+          });
         bq[s][0] = q0 * A.ik0;   // scale0 = keep0 · ik0 (dropped nodes: et = d_in, q = 0)
         bq[s][1] = q1 * A.ik0;
       }
@@ -509,48 +557,55 @@ __global__ void __launch_bounds__(64 * GW) web_gcn_kernel(GcnArgs A) {
           aW0[tb][1] = mfma4(a, bq[s][1], aW0[tb][1]);
         }
     }
-    __syncthreads();   // sD1 / sEt are rewritten by the next instance
   }
   if (!BWD) return;
+  __syncthreads();
 
-  // ---- flush: each wave writes its gradient contributions into its own LDS row,
-  // then the block sums the waves in order into its slab row (deterministic) ----
+  // ---- flush: waves 0-7 store their gradient contributions into LDS rows 0-7,
+  // waves 8-15 add theirs into rows w-8 (every element is owned by one lane of each
+  // wave), then the block sums the 8 rows in order into its slab row (deterministic) ----
   const int C = A.n_gcn;
-  float *row = sm + L.tables + w * C;   // the instance region is dead
-  for (int x = l; x < C; x += 64) row[x] = 0.f;
-  sg_wsync();
+  float *row = sm + L.tables + (w & 7) * C;   // the instance region is dead
+  auto put = [&](int x, float v) {
+    if (w < 8) row[x] = v;
+    else row[x] += v;
+  };
+  for (int pass = 0; pass < 2; ++pass) {
+    if ((w >= 8) == (pass == 1)) {
 #pragma unroll
-  for (int tb = 0; tb < NTB; ++tb)
+      for (int tb = 0; tb < NTB; ++tb)
 #pragma unroll
-    for (int fb = 0; fb < 2; ++fb)
+        for (int fb = 0; fb < 2; ++fb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ty = 16 * tb + 4 * g + r;
-        if (ty < d_in) row[ty * WH1 + 16 * fb + i] = aW0[tb][fb][r];
+          for (int r = 0; r < 4; ++r) {
+            const int ty = 16 * tb + 4 * g + r;
+            if (ty < d_in) put(ty * WH1 + 16 * fb + i, aW0[tb][fb][r]);
+          }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const float v = sgk::xsum32(sgk::xsum16(aB0[cb]));
+        if (g == 0) put(A.ob0 + 16 * cb + i, v);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) put(A.oW1 + (16 * cb + 4 * g + r) * WH2 + i, aW1[cb][r] * A.ik1);
       }
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb) {
-    const float v = sgk::xsum32(sgk::xsum16(aB0[cb]));
-    if (g == 0) row[A.ob0 + 16 * cb + i] = v;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) row[A.oW1 + (16 * cb + 4 * g + r) * WH2 + i] = aW1[cb][r] * A.ik1;
-  }
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const float vb = sgk::row_sum16(aB1[s]);
-    const float vd = sgk::row_sum16(aWd[s]) * A.ik2;
-    if (i == 0) {
-      row[A.ob1 + 4 * g + s] = vb;
-      row[A.oWd + 4 * g + s] = vd;
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const float vb = sgk::row_sum16(aB1[s2]);
+        const float vd = sgk::row_sum16(aWd[s2]) * A.ik2;
+        if (i == 0) {
+          put(A.ob1 + 4 * g + s2, vb);
+          put(A.oWd + 4 * g + s2, vd);
+        }
+      }
+      const float bsum = sg_wave_sum(aBd);
+      if (l == 0) put(A.obd, bsum);
     }
+    __syncthreads();
   }
-  const float bsum = sg_wave_sum(aBd);
-  if (l == 0) row[A.obd] = bsum;
-  __syncthreads();
   float *dst = A.slab + (size_t)blockIdx.x * C;
-  for (int x = tid; x < C; x += 64 * GW) {
+  for (int x = tid; x < C; x += NT) {
     float v = 0.f;
-    for (int u = 0; u < GW; ++u) v += sm[L.tables + u * C + x];
+    for (int uu = 0; uu < 8; ++uu) v += sm[L.tables + uu * C + x];
     dst[x] += v;
   }
 }
@@ -1011,37 +1066,61 @@ static int web_status() {
   return SG_ERR_HIP;
 }
 
-static void gcn_launch(bool bwd, const WebPlan &W, const GcnArgs &A, int blocks, hipStream_t st) {
-  const int n16 = (A.n_max + 15) & ~15;
-  const GcnLds L = gcn_lds(W.d_in, n16, bwd);
+// LDS of the instance kernel; CSR staged in LDS when it fits
+static size_t gcn_lds_bytes(const WebPlan &W, int n_max, int max_nnz, bool bwd, bool lcsr) {
+  const int n16 = (n_max + 15) & ~15;
+  const GcnLds L = gcn_lds(W.d_in, n16, max_nnz, bwd, lcsr);
   size_t lds = (size_t)L.total * 4u;
   if (bwd) {
-    const size_t fl = ((size_t)L.tables + (size_t)GW * W.n_gcn) * 4u;
+    const size_t fl = ((size_t)L.tables + 8u * (size_t)W.n_gcn) * 4u;
     if (fl > lds) lds = fl;
   }
-  const void *fn = nullptr;
-#define SG_WEB_GCN(B, NT)                                                                      \
-  do {                                                                                       \
-    fn = (const void *)web_gcn_kernel<B, NT>;                                                \
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);     \
-    hipLaunchKernelGGL((web_gcn_kernel<B, NT>), dim3(blocks), dim3(64 * GW), lds, st, A);    \
+  return lds;
+}
+
+static int gcn_launch(bool bwd, const WebPlan &W, const GcnArgs &A, int64_t n_inst,
+                      hipStream_t st) {
+  const bool lcsr = gcn_lds_bytes(W, A.n_max, A.max_nnz, bwd, true) <= 163840u;
+  const size_t lds = gcn_lds_bytes(W, A.n_max, A.max_nnz, bwd, lcsr);
+  if (lds > 163840u) return SG_ERR_UNSUPPORTED;
+  int per_cu = (int)(163840u / lds);
+  if (per_cu > 2048 / (64 * gcn_gw(bwd))) per_cu = 2048 / (64 * gcn_gw(bwd));
+  int64_t blocks = (int64_t)sg_num_cus() * per_cu;
+  if (bwd) blocks = sg_num_cus();   // one slab row per block (web_ws sizes the slab for this)
+  if (blocks > n_inst) blocks = n_inst;
+  if (blocks < 1) return SG_OK;
+#define SG_WEB_GCN(B, NT, LC)                                                                   \
+  do {                                                                                        \
+    const void *fn = (const void *)web_gcn_kernel<B, NT, LC>;                                 \
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);      \
+    hipLaunchKernelGGL((web_gcn_kernel<B, NT, LC>), dim3((unsigned)blocks), dim3(64 * gcn_gw(B)), \
+                       lds, st, A);                                                           \
+  } while (0)
+#define SG_WEB_GCN_NT(NT)                             \
+  do {                                                \
+    if (bwd) {                                        \
+      if (lcsr) SG_WEB_GCN(true, NT, true);           \
+      else SG_WEB_GCN(true, NT, false);               \
+    } else {                                          \
+      if (lcsr) SG_WEB_GCN(false, NT, true);          \
+      else SG_WEB_GCN(false, NT, false);              \
+    }                                                 \
   } while (0)
   switch (W.tb) {
-    case 1: if (bwd) SG_WEB_GCN(true, 1); else SG_WEB_GCN(false, 1); break;
-    case 2: if (bwd) SG_WEB_GCN(true, 2); else SG_WEB_GCN(false, 2); break;
-    case 3: if (bwd) SG_WEB_GCN(true, 3); else SG_WEB_GCN(false, 3); break;
-    default: if (bwd) SG_WEB_GCN(true, 4); else SG_WEB_GCN(false, 4); break;
+    case 1: SG_WEB_GCN_NT(1); break;
+    case 2: SG_WEB_GCN_NT(2); break;
+    case 3: SG_WEB_GCN_NT(3); break;
+    default: SG_WEB_GCN_NT(4); break;
   }
+#undef SG_WEB_GCN_NT
 #undef SG_WEB_GCN
+  return SG_OK;
 }
 
 int sg_web_lds_ok(const sg_model_t *m) {
   WebPlan W;
   if (web_plan(m, &W) != SG_OK) return 0;
-  const int n16 = (m->n_max + 15) & ~15;
-  const GcnLds L = gcn_lds(W.d_in, n16, true);
-  const size_t fl = ((size_t)L.tables + (size_t)GW * W.n_gcn) * 4u;
-  return (size_t)L.total * 4u <= 163840u && fl <= 163840u;
+  return gcn_lds_bytes(W, m->n_max, 0, true, false) <= 163840u;
 }
 
 int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *pairs,
@@ -1053,7 +1132,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
   int rc = web_plan(m, &W);
   if (rc != SG_OK) return rc;
   if (!store || !store->node_off || !store->types || !store->row_ptr || !store->col ||
-      !store->val || store->n_max > W.D || store->n_max > m->n_max)
+      !store->val || store->n_max > W.D || store->n_max > m->n_max || store->max_nnz < 0)
     return SG_ERR_ARG;
   if (!sg_web_lds_ok(m)) return SG_ERR_UNSUPPORTED;
   if (chunk <= 0) chunk = n_pairs > 0 ? n_pairs : 1;
@@ -1096,6 +1175,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
   G.ik0 = W.ik0; G.ik1 = W.ik1; G.ik2 = W.ik2; G.ik4 = W.ik4;
   G.padv = W.padv;
   G.d_in = W.d_in; G.D = D; G.Dp = Dp; G.n_gcn = W.n_gcn; G.n_max = store->n_max;
+  G.max_nnz = store->max_nnz;
   G.ob0 = W.ob0; G.oW1 = W.oW1; G.ob1 = W.ob1; G.oWd = W.oWd; G.obd = W.obd;
   HeadArgs H;
   H.X = X; H.T = T; H.params = params; H.labels = labels; H.y_stats = y_stats;
@@ -1116,8 +1196,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     G.pairs = pc;
     G.n_pairs = n;
     G.pair_offset = pair_offset + c0;
-    const int64_t gb = 2 * n < ws.gcn_blocks ? 2 * n : ws.gcn_blocks;
-    gcn_launch(false, W, G, (int)gb, st);
+    if ((rc = gcn_launch(false, W, G, 2 * n, st)) != SG_OK) return rc;
     hipLaunchKernelGGL(web_t_kernel, dim3((unsigned)nblk, Dp / TB, K), dim3(256), 0, st,
                        X + ws.Cp * Dp, Wg,
                        EXT128, n, Dp, K, T);
@@ -1133,7 +1212,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
                          st, X, X + ws.Cp * Dp, GM, EXT16, n, Dp, K, GWS);
       hipLaunchKernelGGL(web_gv_kernel, dim3(2 * Dp / 64, WSPLIT), dim3(256), 0, st, X, GM, n,
                          ws.Cp, Dp, K, GVS);
-      gcn_launch(true, W, G, ws.gcn_blocks, st);
+      if ((rc = gcn_launch(true, W, G, 2 * n, st)) != SG_OK) return rc;
     } else {
       hipLaunchKernelGGL(web_head_kernel<false>, dim3(hb), dim3(256), head_lds, st, H);
     }

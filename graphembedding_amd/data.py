@@ -145,6 +145,9 @@ SYNTHETIC = {
     'syn_aids10knef': (10000, 18, 5, 30, 29),
     'syn_web': (1000, 100, 64, 512, 29),
 }
+# mean extra-edge degree of the sparse synthetic sets (p_extra = deg / (n - 1));
+# the others use p_extra = 0.15 (AIDS-like density)
+SYNTHETIC_EXTRA_DEGREE = {'syn_web': 4.0}
 
 
 def synthetic_graph(rng: np.random.Generator, n: int, gid: int, n_types: int = 29,
@@ -172,10 +175,12 @@ def synthetic_graph(rng: np.random.Generator, n: int, gid: int, n_types: int = 2
 def synthetic_graphs(name: str, seed: int = 123):
     n_train, n_test, lo, hi, nt = SYNTHETIC[name]
     rng = np.random.default_rng(seed)
+    deg = SYNTHETIC_EXTRA_DEGREE.get(name)
     gs = []
     for gid in range(n_train + n_test):
         n = int(rng.integers(lo, hi + 1))
-        gs.append(synthetic_graph(rng, n, gid, nt))
+        pe = 0.15 if deg is None else min(0.15, deg / max(n - 1, 1))
+        gs.append(synthetic_graph(rng, n, gid, nt, p_extra=pe))
     return gs[:n_train], gs[n_train:]
 
 

@@ -66,6 +66,7 @@ class CsrStore(object):
         self.col = np.concatenate(cols) if cols else np.zeros(0, np.int32)
         self.val = np.concatenate(vals) if vals else np.zeros(0, np.float32)
         self.n_max = int(ns.max()) if G else 1
+        self.max_nnz = int(np.diff(self.row_ptr[self.node_off]).max()) if G else 0
         self.gids = [mg.nxgraph.graph.get('gid') for mg in model_graphs]
         self._dev = None
         self._struct = None
@@ -86,7 +87,8 @@ class CsrStore(object):
             self._dev = (t(self.node_off), t(self.types), t(self.row_ptr),
                          t(self.col if self.col.size else np.zeros(1, np.int32)),
                          t(self.val if self.val.size else np.zeros(1, np.float32)))
-            self._struct = _lib.csr_struct(len(self), self.n_max, *self._dev)
+            self._struct = _lib.csr_struct(len(self), self.n_max, *self._dev,
+                                           max_nnz=self.max_nnz)
         return self._struct
 
 

@@ -265,6 +265,7 @@ int32_t sg_sampler_density(int32_t *state, const int32_t *dens_order, const int3
  *   row_ptr  [n_nodes + 1]   CSR row offsets of Â (graphs.py:64-76) into col/val
  *   col      [nnz]           neighbour as a node index LOCAL to its graph
  *   val      [nnz]           Â entry (f32 cast of the reference's float64, A11)
+ *   max_nnz                  largest Â entry count of one graph (LDS staging size)
  * Â must be symmetric (undirected graphs, as the reference's).  Every graph
  * must have 1 <= n <= n_max <= D nodes (tf.pad, quirk A9), checked by the host.
  */
@@ -276,6 +277,7 @@ typedef struct sg_csr_store {
   const int32_t *row_ptr;
   const int32_t *col;
   const float *val;
+  int32_t max_nnz;
 } sg_csr_store_t;
 
 /* Workspace bytes for sg_web_forward / sg_web_fwd_bwd processing chunks of up

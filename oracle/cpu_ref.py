@@ -113,3 +113,39 @@ def time_allpairs_sample(gs, labels, flags, n_sample: int = 0, target_s: float =
             'kind': 'port',
             'sample': '{}, fwd+bwd (loss + grads, no Adam), C restatement oracle/siamese_cpu.c, '
                       'fp32, OpenMP {} threads, {:.1f} s'.format(what, threads, dt)}
+
+
+def time_web_sample(gs, labels, flags, n_sample: int = 32, target_s: float = 12.0,
+                    threads: int = 0, seed: int = 0):
+    """Config C5 (Web-sized graphs): time the C restatement on a seeded random
+    sample of n_sample pairs of the all-pairs stream, packed as dense records at
+    capacity n_max = D (the port has no sparse path), repeated for ~target_s."""
+    from graphembedding_amd.model_mse import glorot_flat
+    from graphembedding_amd.layers_factory import create_layers
+    from graphembedding_amd.packer import GraphStore
+    G = len(gs.graphs)
+    threads = threads if threads and threads > 0 else default_threads()
+    layers = create_layers(flags, gs.d_in)
+    params = glorot_flat(layers, gs.d_in, flags.param_seed)
+    ybar = float(labels.astype(np.float64).mean())
+    rng = np.random.default_rng(seed)
+    p = rng.choice(G * G, size=n_sample, replace=False)
+    pairs = np.stack([p // G, p % G], axis=1)
+    uniq, inv = np.unique(pairs.reshape(-1), return_inverse=True)
+    store = GraphStore([gs.mgs[i] for i in uniq], gs.n_max, gs.d_in)
+    words = store.pack_host(inv.reshape(-1, 2), labels.reshape(-1)[p])
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        fwd_bwd_records(words, gs.n_max, gs.d_in, params, 1 + reps, 1.0 - flags.dropout,
+                        flags.yeta, ybar, threads=threads)
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= target_s:
+            break
+    return {'value': n_sample * reps / dt, 'unit': 'graph-pairs/s', 'cores': threads,
+            'kind': 'port',
+            'sample': '{} x {} random pairs of the all-pairs stream (seed {}), fwd+bwd (loss + '
+                      'grads, no Adam), C restatement oracle/siamese_cpu.c on dense capacity-{} '
+                      'records, fp32, OpenMP {} threads, {:.1f} s'.format(
+                          reps, n_sample, seed, gs.n_max, threads, dt)}
