@@ -1,0 +1,78 @@
+"""CPU tests of the graph-store path's host side (config C5): model validation
+routes Web-sized stacks to path 3, the CSR store reproduces Â and the one-hot
+columns exactly, the size ordering and rank shards partition the all-pairs list,
+and the workspace / LDS sizing calls are host-only."""
+import numpy as np
+import pytest
+
+from _fixtures import small_problem
+from graphembedding_amd import _lib
+from graphembedding_amd.web import CsrStore, WebAllPairs, allpairs_ids, size_order
+
+
+def _model(prob, n_max, **kw):
+    return _lib.make_model(prob.layers, prob.d_in, n_max, 0.9, 'sim_kernel', 'gaussian', 0.6,
+                           **kw)
+
+
+@pytest.mark.parametrize('D', [32, 64, 200, 512])
+def test_web_stacks_take_path_3(D):
+    prob = small_problem(n_graphs=4, n_pairs=4, seed=2, n_lo=5, n_hi=min(D, 40), n_max=D)
+    n, path = _lib.validate(_model(prob, D))
+    assert path == _lib.PATH_WEB
+    assert n == prob.d_in * 32 + 32 + 32 * 16 + 16 + 16 + 1 + D * D * 10 + 10 * 2 * D + 10 + 10
+    assert _lib.web_workspace_bytes(_model(prob, D), 1000) > 0
+
+
+def test_web_path_limits():
+    prob = small_problem(n_graphs=4, n_pairs=4, seed=2, n_lo=5, n_hi=30, n_max=30)
+    assert _lib.validate(_model(prob, 32))[1] == 2            # C4 capacity-32 kernel
+    big = small_problem(n_graphs=2, n_pairs=2, seed=2, n_lo=5, n_hi=30, n_max=520)
+    with pytest.raises(_lib.SiameseHipError):                  # D > 512: no kernel
+        _lib.validate(_model(big, 520))
+    mid = small_problem(n_graphs=2, n_pairs=2, seed=2, n_lo=5, n_hi=30, n_max=64)
+    with pytest.raises(_lib.SiameseHipError):                  # N > max_in_dims (A9)
+        _lib.validate(_model(mid, 65))
+
+
+def test_csr_store_reproduces_adjacency():
+    prob = small_problem(n_graphs=9, n_pairs=4, seed=6, n_lo=1, n_hi=70, n_max=128,
+                         p_extra=0.05)
+    st = CsrStore(prob.mgs, prob.d_in, 128)
+    assert st.node_off[-1] == sum(m.num_nodes() for m in prob.mgs)
+    for g, mg in enumerate(prob.mgs):
+        o, n = int(st.node_off[g]), int(st.n[g])
+        A = np.zeros((n, n), np.float32)
+        for r in range(n):
+            e0, e1 = st.row_ptr[o + r], st.row_ptr[o + r + 1]
+            A[r, st.col[e0:e1]] = st.val[e0:e1]
+        assert np.array_equal(A, mg.adj.astype(np.float32))
+        assert np.array_equal(st.types[o:o + n], mg.types)
+    assert st.max_nnz == max(int(np.count_nonzero(m.adj)) for m in prob.mgs)
+    with pytest.raises(RuntimeError):
+        CsrStore(prob.mgs, prob.d_in, 10)                      # tf.pad: N > max_in_dims
+
+
+def test_size_order_and_shards():
+    n_nodes = np.array([300, 64, 500, 64, 120], np.int32)
+    ids = allpairs_ids(5, 0, 25)
+    order = size_order(ids, n_nodes)
+    assert sorted(order.tolist()) == list(range(25))
+    key = (n_nodes[ids[order, 0]] // 32) * 64 + n_nodes[ids[order, 1]] // 32
+    assert np.all(np.diff(key) >= 0)
+
+
+def test_web_allpairs_shards_partition_the_list():
+    from types import SimpleNamespace
+    prob = small_problem(n_graphs=7, n_pairs=2, seed=4, n_lo=3, n_hi=60, n_max=64)
+    gs = SimpleNamespace(graphs=prob.graphs, mgs=prob.mgs, d_in=prob.d_in)
+    labels = np.arange(49, dtype=np.float32).reshape(7, 7) / 49
+    full = WebAllPairs(gs, labels, 0, 1, device='cpu')
+    parts = [WebAllPairs(gs, labels, r, 3, device='cpu') for r in range(3)]
+    assert sum(p.n for p in parts) == 49
+    cat = np.concatenate([p.pairs.numpy() for p in parts])
+    assert np.array_equal(cat, full.pairs.numpy())
+    lab = np.concatenate([p.labels.numpy() for p in parts])
+    assert np.array_equal(lab, labels[cat[:, 0], cat[:, 1]])
+    assert all(np.allclose(p.y_stats.numpy(), full.y_stats.numpy()) for p in parts)
+    assert [p.start for p in parts] == [0, parts[0].end, parts[1].end]
