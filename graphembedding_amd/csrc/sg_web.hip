@@ -30,6 +30,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "sg_common.h"
 #include "sg_mfma.h"
 
@@ -130,7 +132,7 @@ int web_plan(const sg_model_t *m, WebPlan *W) {
 // ---------------------------------------------------------------------------
 struct WebWs {
   int64_t Cp;                                        // chunk rounded up to TB
-  int64_t X, GX, T, GM, EXT, EXT16, EXT128;          // per-chunk buffers
+  int64_t X, GX, T, GM, EXT, EXT16, EXT128, INST;    // per-chunk buffers
   int64_t Wg, Wh, GWS, GVS, GSLAB, HSLABo, total;    // per-call buffers
   int gcn_blocks, head_blocks;
 };
@@ -152,6 +154,7 @@ WebWs web_ws(const WebPlan &W, int64_t chunk) {
   w.EXT = take(2 * w.Cp);           // int2 per pair
   w.EXT16 = take(2 * (w.Cp / 16));
   w.EXT128 = take(2 * (w.Cp / TB));
+  w.INST = take(8 * w.Cp);          // int4 per instance
   w.Wg = take(K * Dp * Dp);
   w.Wh = take(K * Dp * Dp);
   w.GWS = take((int64_t)WSPLIT * K * Dp * Dp);
@@ -170,16 +173,24 @@ WebWs web_ws(const WebPlan &W, int64_t chunk) {
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(TB) web_ext_kernel(const int32_t *__restrict__ pairs, int64_t n,
                                                      const int32_t *__restrict__ node_off,
+                                                     const int32_t *__restrict__ row_ptr,
                                                      int full, int D, int2 *__restrict__ ext,
                                                      int2 *__restrict__ ext16,
-                                                     int2 *__restrict__ ext128) {
+                                                     int2 *__restrict__ ext128,
+                                                     int4 *__restrict__ inst) {
   __shared__ int2 red[2];
   const int64_t p = (int64_t)blockIdx.x * TB + threadIdx.x;
   int e1 = 0, e2 = 0;
   if (p < n) {
     const int g1 = pairs[2 * p], g2 = pairs[2 * p + 1];
-    e1 = full ? D : node_off[g1 + 1] - node_off[g1];
-    e2 = full ? D : node_off[g2 + 1] - node_off[g2];
+    const int o1 = node_off[g1], n1 = node_off[g1 + 1] - o1;
+    const int o2 = node_off[g2], n2 = node_off[g2 + 1] - o2;
+    e1 = full ? D : n1;
+    e2 = full ? D : n2;
+    // per-instance (first node, nodes, first Â entry, Â entries) for web_gcn_kernel
+    const int b1 = row_ptr[o1], b2 = row_ptr[o2];
+    inst[2 * p] = make_int4(o1, n1, b1, row_ptr[o1 + n1] - b1);
+    inst[2 * p + 1] = make_int4(o2, n2, b2, row_ptr[o2 + n2] - b2);
   }
   ext[p] = make_int2(e1, e2);
   int m1 = e1, m2 = e2;
@@ -249,6 +260,7 @@ struct GcnArgs {
   const int32_t *node_off, *types, *row_ptr, *col;
   const float *val;
   const int32_t *pairs;
+  const int4 *inst;  // [2 n_pairs] (first node, nodes, first Â entry, Â entries) per instance
   int64_t n_pairs, pair_offset, Cp;
   const float *params;
   float *X;          // [2][Cp][Dp] NTN inputs (forward)
@@ -268,14 +280,18 @@ struct GcnArgs {
 //   sD1 [N16][32] (backward): D1' = H1·m1, then gP0,
 //   sScr [8 waves][16][16] (backward): a wave's gS1 tile, re-read as MFMA B operand,
 //   CSR (LCSR): row offsets [N16 + 1], columns [max_nnz], values [max_nnz].
+// LDS row strides (words): not multiples of 16, so the random-row b128 gathers of
+// the sparse products spread over the banks (stride 16 puts every row on 4 bank groups)
+constexpr int W0S = 36, ZS = 20, DS = 36;
+
 struct GcnLds {
-  int w0, b0, w1, w1t, b1, wd, tables, et, z1, d1, scr, rp, col, val, total;
+  int w0, b0, w1, w1t, b1, wd, tables, et, gx, z1, d1, scr, rp, col, val, total;
 };
 
 __host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, int max_nnz, bool bwd, bool lcsr) {
   GcnLds L;
   int o = 0;
-  L.w0 = o; o += (d_in + 1) * WH1;
+  L.w0 = o; o += (d_in + 1) * W0S;
   L.b0 = o; o += WH1;
   L.w1 = o; o += WH1 * WH2;
   L.w1t = o; o += WH1 * WH2;
@@ -284,19 +300,20 @@ __host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, int max_nnz, bool b
   o = (o + 3) & ~3;
   L.tables = o;
   L.et = o; o += n16;
-  L.z1 = o; o += n16 * WH2;
-  L.d1 = o; if (bwd) o += n16 * WH1;
+  L.gx = o; if (bwd) o += n16;
+  L.z1 = o; o += n16 * ZS;
+  L.d1 = o; if (bwd) o += n16 * DS;
   L.scr = o; if (bwd) o += gcn_gw(true) * 256;
   L.rp = o; if (lcsr) o += (n16 + 4) & ~3;
-  L.col = o; if (lcsr) o += (max_nnz + 3) & ~3;
+  L.col = o; if (lcsr) o += ((max_nnz + 1) / 2 + 3) & ~3;   // u16 columns
   L.val = o; if (lcsr) o += (max_nnz + 3) & ~3;
   L.total = o;
   return L;
 }
 
 // Σ_e val[e] · f(col[e]) over one CSR row, four neighbours' loads in flight at a time
-template <typename F>
-__device__ __forceinline__ void csr_row(const int *__restrict__ col, const float *__restrict__ val,
+template <typename CT, typename F>
+__device__ __forceinline__ void csr_row(const CT *__restrict__ col, const float *__restrict__ val,
                                         int e0, int e1, F f) {
   int e = e0;
   for (; e + 4 <= e1; e += 4) {
@@ -312,6 +329,7 @@ __device__ __forceinline__ void csr_row(const int *__restrict__ col, const float
 
 template <bool BWD, int NTB, bool LCSR>
 __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
+  using ColT = typename std::conditional<LCSR, uint16_t, int>::type;
   constexpr int GW_ = gcn_gw(BWD), NT = 64 * GW_, GCN_TPW = 32 / GW_;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
@@ -323,10 +341,12 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
   float *sb1 = sm + L.b1, *sWd = sm + L.wd;
   int *sEt = (int *)(sm + L.et);
   float *sZ1 = sm + L.z1, *sD1 = sm + L.d1, *scr = sm + L.scr + w * 256;
-  int *sRp = (int *)(sm + L.rp), *sCol = (int *)(sm + L.col);
+  int *sRp = (int *)(sm + L.rp);
+  uint16_t *sCol = (uint16_t *)(sm + L.col);
   float *sVal = sm + L.val;
   const float *prm = A.params;
-  for (int x = tid; x < (d_in + 1) * WH1; x += NT) sW0[x] = x < d_in * WH1 ? prm[x] * A.ik0 : 0.f;
+  for (int x = tid; x < (d_in + 1) * WH1; x += NT)
+    sW0[(x / WH1) * W0S + x % WH1] = x < d_in * WH1 ? prm[x] * A.ik0 : 0.f;
   for (int x = tid; x < WH1 * WH2; x += NT) {
     const float v = prm[A.oW1 + x] * A.ik1;
     sW1[x] = v;
@@ -347,34 +367,65 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
   for (int t = 0; t < NTB; ++t) aW0[t][0] = aW0[t][1] = f4{0.f, 0.f, 0.f, 0.f};
   aW1[0] = aW1[1] = f4{0.f, 0.f, 0.f, 0.f};
 
+  // The next instance's inputs are prefetched into registers while this one computes:
+  // its (o, N, eb, nnz) at the top of the iteration, its rows after the first phase.
+  constexpr int KM = LCSR ? 4096 / NT : 1;   // CSR entries per thread (LCSR: nnz <= 4096)
+  int pr_rp = 0, pr_ty = 0, pr_col[KM];
+  float pr_val[KM], pr_gx = 0.f;
+  auto load_rows = [&](int64_t q, int4 in) {
+    const int o = in.x, N = in.y, eb = in.z, nnz = in.w;
+    pr_rp = tid < N ? A.row_ptr[o + tid] - eb : 0;
+    pr_ty = tid < N ? A.types[o + tid] : 0;
+    if (BWD)
+      pr_gx = tid < N ? A.GX[((int64_t)(q & 1) * A.Cp + (q >> 1)) * A.Dp + tid] : 0.f;
+    if (LCSR) {
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        const int e = tid + k * NT;
+        pr_col[k] = e < nnz ? A.col[eb + e] : 0;
+        pr_val[k] = e < nnz ? A.val[eb + e] : 0.f;
+      }
+    }
+  };
   const int64_t n_inst = 2 * A.n_pairs;
+  int4 in = make_int4(0, 0, 0, 0);
+  if ((int64_t)blockIdx.x < n_inst) {
+    in = A.inst[blockIdx.x];
+    load_rows(blockIdx.x, in);
+  }
   for (int64_t q = blockIdx.x; q < n_inst; q += gridDim.x) {
     __syncthreads();   // the previous instance (or the table build) is done with the LDS
     const int64_t p = q >> 1;
     const int side = (int)(q & 1);
-    const int gid = A.pairs[2 * p + side];
-    const int o = A.node_off[gid];
-    const int N = A.node_off[gid + 1] - o;
+    const int o = in.x, N = in.y;
     const int n16 = (N + 15) & ~15;
     const int ntile = n16 >> 4;
     const uint32_t pk = sg_pair_key(A.key, (uint32_t)(A.pair_offset + p));
     const int *rp;
-    const int *cl;
+    const ColT *cl;
     const float *vl;
+    // stage the prefetched rows; effective one-hot column per node (sparse dropout of
+    // X, layer 0, e = node: d_in = the zero row of sW0 for dropped and absent nodes)
+    if (tid < n16)
+      sEt[tid] = (tid < N && sg_keep(pk, 0, side, tid, A.thr0)) ? pr_ty : d_in;
+    if (BWD && tid < n16) sm[L.gx + tid] = pr_gx;
     if (LCSR) {
-      const int eb = A.row_ptr[o], nnz = A.row_ptr[o + N] - eb;
-      for (int n = tid; n <= N; n += NT) sRp[n] = A.row_ptr[o + n] - eb;
-      for (int e = tid; e < nnz; e += NT) {
-        sCol[e] = A.col[eb + e];
-        sVal[e] = A.val[eb + e];
+      if (tid < N) sRp[tid] = pr_rp;
+      if (tid == 0) sRp[N] = in.w;
+#pragma unroll
+      for (int k = 0; k < KM; ++k) {
+        const int e = tid + k * NT;
+        if (e < in.w) {
+          sCol[e] = (uint16_t)pr_col[k];
+          sVal[e] = pr_val[k];
+        }
       }
-      rp = sRp; cl = sCol; vl = sVal;
+      rp = sRp; cl = (const ColT *)(const void *)sCol; vl = sVal;
     } else {
-      rp = A.row_ptr + o; cl = A.col; vl = A.val;
+      rp = A.row_ptr + o; cl = (const ColT *)(const void *)A.col; vl = A.val;
     }
-    // effective one-hot column per node (sparse dropout of X, layer 0, e = node)
-    for (int n = tid; n < n16; n += NT)
-      sEt[n] = (n < N && sg_keep(pk, 0, side, n, A.thr0)) ? A.types[o + n] : d_in;
+    const int64_t qn = q + gridDim.x;
+    const int4 inn = qn < n_inst ? A.inst[qn] : make_int4(0, 0, 0, 0);
     __syncthreads();
 
     // ---- forward: H1 (lane (i, g): node 16t+i, features 16c + 4g + s), D1', Z1 ----
@@ -391,7 +442,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
       }
       if (n < N) {
         csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
-          const float *wr = sW0 + sEt[mm] * WH1 + 4 * g;
+          const float *wr = sW0 + sEt[mm] * W0S + 4 * g;
           const float4 wa = *(const float4 *)wr, wb = *(const float4 *)(wr + 16);
           h[0] = fmaf(v, wa.x, h[0]); h[1] = fmaf(v, wa.y, h[1]);
           h[2] = fmaf(v, wa.z, h[2]); h[3] = fmaf(v, wa.w, h[3]);
@@ -416,13 +467,14 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) z = mfma4(h[4 * c + s], sW1[(16 * c + 4 * g + s) * WH2 + i], z);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sZ1[(16 * t + 4 * g + r) * WH2 + i] = z[r];
+      for (int r = 0; r < 4; ++r) sZ1[(16 * t + 4 * g + r) * ZS + i] = z[r];
       if (BWD) {
-        *(float4 *)(sD1 + n * WH1 + 4 * g) = make_float4(h[0], h[1], h[2], h[3]);
-        *(float4 *)(sD1 + n * WH1 + 16 + 4 * g) = make_float4(h[4], h[5], h[6], h[7]);
+        *(float4 *)(sD1 + n * DS + 4 * g) = make_float4(h[0], h[1], h[2], h[3]);
+        *(float4 *)(sD1 + n * DS + 16 + 4 * g) = make_float4(h[4], h[5], h[6], h[7]);
       }
     }
     __syncthreads();
+    if (qn < n_inst) load_rows(qn, inn);   // lands during the rest of this instance
 
     // ---- H2 (lane (i, g): node 16t+i, features 4g..4g+3), Dense, Padding, NTN input ----
     float gzr[GCN_TPW][4];
@@ -436,7 +488,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
         const float4 b = *(const float4 *)(sb1 + 4 * g);
         h2[0] = b.x; h2[1] = b.y; h2[2] = b.z; h2[3] = b.w;
         csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
-          const float4 zz = *(const float4 *)(sZ1 + mm * WH2 + 4 * g);
+          const float4 zz = *(const float4 *)(sZ1 + mm * ZS + 4 * g);
           h2[0] = fmaf(v, zz.x, h2[0]); h2[1] = fmaf(v, zz.y, h2[1]);
           h2[2] = fmaf(v, zz.z, h2[2]); h2[3] = fmaf(v, zz.w, h2[3]);
         });
@@ -456,7 +508,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
           A.X[((int64_t)side * A.Cp + p) * A.Dp + n] = k4 ? z * A.ik4 : 0.f;
       } else {
         // Dense / Padding / NTN-input backward: gZ1 (= gH2, identity act) in registers
-        const float gx = k4 ? A.GX[((int64_t)side * A.Cp + p) * A.Dp + n] * A.ik4 : 0.f;
+        const float gx = k4 ? sm[L.gx + n] * A.ik4 : 0.f;
         const float gp = (n < N && pre > 0.f) ? gx : 0.f;
         if (g == 0) aBd += gp;
 #pragma unroll
@@ -473,6 +525,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
         A.X[((int64_t)side * A.Cp + p) * A.Dp + a] =
             (a < A.D && A.padv != 0.f && sg_keep(pk, 4, side, (uint32_t)a, A.thr4))
                 ? A.padv * A.ik4 : 0.f;
+      in = inn;
       continue;
     }
     __syncthreads();   // every wave is done reading Z1: it becomes gZ1
@@ -480,7 +533,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
     for (int u = 0; u < GCN_TPW; ++u) {
       const int t = w + u * GW_;
       if (t >= ntile) break;
-      *(float4 *)(sZ1 + (16 * t + i) * WH2 + 4 * g) =
+      *(float4 *)(sZ1 + (16 * t + i) * ZS + 4 * g) =
           make_float4(gzr[u][0], gzr[u][1], gzr[u][2], gzr[u][3]);
     }
     __syncthreads();
@@ -494,7 +547,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
       float q4[4] = {0.f, 0.f, 0.f, 0.f};
       if (n < N)
         csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
-          const float4 gg = *(const float4 *)(sZ1 + mm * WH2 + 4 * g);
+          const float4 gg = *(const float4 *)(sZ1 + mm * ZS + 4 * g);
           q4[0] = fmaf(v, gg.x, q4[0]); q4[1] = fmaf(v, gg.y, q4[1]);
           q4[2] = fmaf(v, gg.z, q4[2]); q4[3] = fmaf(v, gg.w, q4[3]);
         });
@@ -512,7 +565,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
         const int nn = 16 * t + 4 * g + s;
         const float b = scr[(4 * g + s) * WH2 + i];
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) aW1[cb] = mfma4(sD1[nn * WH1 + 16 * cb + i], b, aW1[cb]);
+        for (int cb = 0; cb < 2; ++cb) aW1[cb] = mfma4(sD1[nn * DS + 16 * cb + i], b, aW1[cb]);
       }
       sg_wsync();
       // gP0 = relu'·keep·gD1·ik1 = (D1' > 0) · gD1·ik1, in place of D1'
@@ -520,7 +573,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
       for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float *dp = sD1 + (16 * t + 4 * g + r) * WH1 + 16 * cb + i;
+          float *dp = sD1 + (16 * t + 4 * g + r) * DS + 16 * cb + i;
           const float v = *dp > 0.f ? gd[cb][r] : 0.f;
           aB0[cb] += v;
           *dp = v;
@@ -542,8 +595,8 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
         et[s] = sEt[n];
         if (n < N && et[s] < d_in)
           csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
-            q0 = fmaf(v, sD1[mm * WH1 + i], q0);
-            q1 = fmaf(v, sD1[mm * WH1 + 16 + i], q1);
+            q0 = fmaf(v, sD1[mm * DS + i], q0);
+            q1 = fmaf(v, sD1[mm * DS + 16 + i], q1);
           });
         bq[s][0] = q0 * A.ik0;   // scale0 = keep0 · ik0 (dropped nodes: et = d_in, q = 0)
         bq[s][1] = q1 * A.ik0;
@@ -557,6 +610,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
           aW0[tb][1] = mfma4(a, bq[s][1], aW0[tb][1]);
         }
     }
+    in = inn;
   }
   if (!BWD) return;
   __syncthreads();
@@ -1080,7 +1134,8 @@ static size_t gcn_lds_bytes(const WebPlan &W, int n_max, int max_nnz, bool bwd, 
 
 static int gcn_launch(bool bwd, const WebPlan &W, const GcnArgs &A, int64_t n_inst,
                       hipStream_t st) {
-  const bool lcsr = gcn_lds_bytes(W, A.n_max, A.max_nnz, bwd, true) <= 163840u;
+  const bool lcsr = gcn_lds_bytes(W, A.n_max, A.max_nnz, bwd, true) <= 163840u &&
+                    A.max_nnz <= 4096;
   const size_t lds = gcn_lds_bytes(W, A.n_max, A.max_nnz, bwd, lcsr);
   if (lds > 163840u) return SG_ERR_UNSUPPORTED;
   int per_cu = (int)(163840u / lds);
@@ -1142,6 +1197,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
   float *X = base + ws.X, *GX = base + ws.GX, *T = base + ws.T, *GM = base + ws.GM;
   int2 *EXT = (int2 *)(base + ws.EXT), *EXT16 = (int2 *)(base + ws.EXT16);
   int2 *EXT128 = (int2 *)(base + ws.EXT128);
+  int4 *INST = (int4 *)(base + ws.INST);
   float *Wg = base + ws.Wg, *Wh = base + ws.Wh, *GWS = base + ws.GWS, *GVS = base + ws.GVS;
   float *GSLAB = base + ws.GSLAB, *HS = base + ws.HSLABo;
   const int Dp = W.Dp, K = W.K, D = W.D;
@@ -1192,8 +1248,9 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     const int64_t nblk = (n + TB - 1) / TB;
     const int32_t *pc = pairs + 2 * c0;
     hipLaunchKernelGGL(web_ext_kernel, dim3((unsigned)nblk), dim3(TB), 0, st, pc, n,
-                       store->node_off, full, D, EXT, EXT16, EXT128);
+                       store->node_off, store->row_ptr, full, D, EXT, EXT16, EXT128, INST);
     G.pairs = pc;
+    G.inst = INST;
     G.n_pairs = n;
     G.pair_offset = pair_offset + c0;
     if ((rc = gcn_launch(false, W, G, 2 * n, st)) != SG_OK) return rc;
