@@ -58,6 +58,22 @@ def test_web_matches_oracle(gpu, name):
     assert np.array_equal(s2.astype(np.float32), s)
 
 
+def test_web_wide_types_and_k16(gpu):
+    """d_in up to 64 (four one-hot type tiles in the gW0 product), K = 16 NTN maps,
+    a 512-node graph (the largest instance the kernels take)."""
+    ov = dict(layer_3='Padding:max_in_dims=512,padding_value=0',
+              layer_4='NTN:input_dim=512,feature_map_dim=16,inneract=relu,dropout=True,bias=True')
+    prob = small_problem(n_graphs=4, n_pairs=6, seed=17, n_lo=500, n_hi=512, n_max=512,
+                         n_types=60, flags_overrides=ov, p_extra=0.01)
+    assert prob.d_in > 48, prob.d_in
+    model, batch = prob.make_gpu_web_model(device=gpu)
+    ref = run_oracle_step(prob, 99)
+    np.testing.assert_allclose(model.pred_sim_without_act(batch, seed=99).cpu().numpy(), ref.s,
+                               rtol=TOL, atol=TOL)
+    model.fwd_bwd(batch, seed=99)
+    _check_grad(model.grad.cpu().numpy(), ref.grad_mse)
+
+
 def test_web_padding_value(gpu):
     """Non-zero padding_value: the NTN input is non-zero past the graph's nodes, so
     the kernels run the full D extent."""
