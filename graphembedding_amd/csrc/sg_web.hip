@@ -838,28 +838,61 @@ __global__ void __launch_bounds__(256) web_wgrad_kernel(const float *__restrict_
   const int64_t c0 = nc * s / WSPLIT, c1 = nc * (s + 1) / WSPLIT;
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, i = l & 15, g = l >> 4;
   const int wm = w >> 1, wn = w & 1;
-  Tile T;
-  T.zero();
-  for (int64_t c = c0; c < c1; ++c) {
-    const int2 e = ext16[c];
-    if (e.x <= a0 || e.y <= b0) continue;   // every pair of the chunk is zero on this tile
+  // Active 16-pair chunks (some pair reaches this tile) are compacted in order into
+  // an LDS list, a window of 1024 raw chunks at a time, so the main loop can
+  // prefetch the next active chunk into registers while the current one computes.
+  __shared__ int act[1024];
+  __shared__ int wcnt[4];
+  auto stage = [&](float4 (&ra)[2], float4 (&rb)[2], int64_t c) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int q = tid + 256 * u, r = q >> 5, cc = (q & 31) * 4;
       const int64_t p = c * 16 + r;
-      float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+      ra[u] = rb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (p < n) {
         const float gm = GM[p * WKP + k];
         const float4 x = *(const float4 *)(X1 + p * Dp + a0 + cc);
-        va = make_float4(gm * x.x, gm * x.y, gm * x.z, gm * x.w);
-        vb = *(const float4 *)(X2 + p * Dp + b0 + cc);
+        ra[u] = make_float4(gm * x.x, gm * x.y, gm * x.z, gm * x.w);
+        rb[u] = *(const float4 *)(X2 + p * Dp + b0 + cc);
       }
-      *(float4 *)(sA + r * KMS + cc) = va;
-      *(float4 *)(sB + r * KMS + cc) = vb;
     }
-    __syncthreads();
-    mma_km_km(T, sA, sB, wm, wn, i, g);
-    __syncthreads();
+  };
+  Tile T;
+  T.zero();
+  for (int64_t wbase = c0; wbase < c1; wbase += 1024) {
+    int na = 0;
+    for (int r0 = 0; r0 < 1024 && wbase + r0 < c1; r0 += 256) {
+      const int64_t c = wbase + r0 + tid;
+      bool on = false;
+      if (c < c1) {
+        const int2 e = ext16[c];
+        on = e.x > a0 && e.y > b0;
+      }
+      const uint64_t bal = __ballot(on);
+      const int before = __popcll(bal & ((1ull << l) - 1ull));
+      if (l == 0) wcnt[w] = __popcll(bal);
+      __syncthreads();
+      int off = na;
+      for (int u = 0; u < w; ++u) off += wcnt[u];
+      if (on) act[off + before] = (int)(r0 + tid);
+      na += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+      __syncthreads();
+    }
+    if (na == 0) continue;
+    float4 ra[2], rb[2];
+    stage(ra, rb, wbase + act[0]);
+    for (int x = 0; x < na; ++x) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int q = tid + 256 * u, r = q >> 5, cc = (q & 31) * 4;
+        *(float4 *)(sA + r * KMS + cc) = ra[u];
+        *(float4 *)(sB + r * KMS + cc) = rb[u];
+      }
+      __syncthreads();
+      if (x + 1 < na) stage(ra, rb, wbase + act[x + 1]);
+      mma_km_km(T, sA, sB, wm, wn, i, g);
+      __syncthreads();
+    }
   }
   float *base = GWS + (((size_t)s * K + k) * Dp) * Dp;
 #pragma unroll
