@@ -102,6 +102,28 @@ def size_order(pairs: np.ndarray, n_nodes: np.ndarray, bucket: int = 32) -> np.n
     return np.lexsort((b2, b1)).astype(np.int64)
 
 
+def dealt_size_order(pairs: np.ndarray, n_nodes: np.ndarray, block: int = 128,
+                     virtual: int = 8, seed: int = 0) -> np.ndarray:
+    """size_order, cut into `block`-pair blocks (size-homogeneous for the GEMM
+    tiles), then dealt stratified into `virtual` contiguous groups: each run of
+    `virtual` consecutive (similar-cost) blocks gives one block, in a fixed
+    pseudo-random assignment, to every group.  Any contiguous rank shard for a world
+    size dividing `virtual` then holds the same size mix.  Independent of the world
+    size, so the list position (the dropout key) of a pair is too."""
+    order = size_order(pairs, n_nodes)
+    nb = (order.size + block - 1) // block
+    if nb == 0:
+        return order
+    rng = np.random.default_rng(seed)
+    groups = [[] for _ in range(virtual)]
+    for s0 in range(0, nb, virtual):
+        run = np.arange(s0, min(s0 + virtual, nb))
+        dest = rng.permutation(virtual)[:run.size]
+        for b, v in zip(run, dest):
+            groups[v].append(b)
+    return np.concatenate([order[b * block:(b + 1) * block] for g in groups for b in g])
+
+
 def allpairs_ids(G: int, start: int, end: int) -> np.ndarray:
     p = np.arange(start, end, dtype=np.int64)
     return np.stack([p // G, p % G], axis=1).astype(np.int32)
@@ -110,10 +132,11 @@ def allpairs_ids(G: int, start: int, end: int) -> np.ndarray:
 class WebAllPairs(object):
     """This rank's shard of the all-pairs stream on the graph store.
 
-    The ordered pair space of G graphs is first sorted by size bucket (once, on
-    the host: the same permutation on every rank), then split into contiguous
-    rank shards; list position = dropout key, so a sharded step computes the
-    unsharded one.  Labels stay on the device with the pair ids.
+    The ordered pair space of G graphs is ordered once on the host by
+    dealt_size_order (the same permutation on every rank and for every world
+    size), then split into contiguous rank shards with equal size mixes; list
+    position = dropout key, so a sharded step computes the unsharded one.  Labels
+    stay on the device with the pair ids.
     """
 
     def __init__(self, gs, labels: np.ndarray, rank: int = 0, world: int = 1, device='cuda',
@@ -124,7 +147,7 @@ class WebAllPairs(object):
         self.total = int(n_pairs if n_pairs is not None else G * G)
         self.store = CsrStore(gs.mgs, d_in if d_in is not None else gs.d_in, n_cap)
         ids = allpairs_ids(G, 0, self.total)
-        order = size_order(ids, self.store.n)
+        order = dealt_size_order(ids, self.store.n)
         ids = ids[order]
         flat = labels.reshape(-1)[:self.total][order]
         self.start, self.end = shard_range(self.total, rank, world)

@@ -7,7 +7,8 @@ import pytest
 
 from _fixtures import small_problem
 from graphembedding_amd import _lib
-from graphembedding_amd.web import CsrStore, WebAllPairs, allpairs_ids, size_order
+from graphembedding_amd.web import (CsrStore, WebAllPairs, allpairs_ids, dealt_size_order,
+                                    size_order)
 
 
 def _model(prob, n_max, **kw):
@@ -60,6 +61,22 @@ def test_size_order_and_shards():
     assert sorted(order.tolist()) == list(range(25))
     key = (n_nodes[ids[order, 0]] // 32) * 64 + n_nodes[ids[order, 1]] // 32
     assert np.all(np.diff(key) >= 0)
+
+
+def test_dealt_order_balances_shards():
+    rng = np.random.default_rng(0)
+    G = 600
+    n_nodes = rng.integers(64, 513, size=G).astype(np.int32)
+    P = G * G
+    ids = allpairs_ids(G, 0, P)
+    order = dealt_size_order(ids, n_nodes)
+    assert np.array_equal(np.sort(order), np.arange(P))
+    cost = (n_nodes[ids[order, 0]].astype(np.float64) * n_nodes[ids[order, 1]])
+    for W in (2, 4, 8):
+        per = [cost[r * P // W:(r + 1) * P // W].sum() for r in range(W)]
+        assert max(per) / min(per) < 1.03, (W, per)
+    b1 = (n_nodes[ids[order[:128 * 64], 0]] // 32).reshape(-1, 128)
+    assert np.mean(b1.max(1) - b1.min(1) <= 1) > 0.9   # blocks stay size-homogeneous
 
 
 def test_web_allpairs_shards_partition_the_list():
