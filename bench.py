@@ -50,6 +50,9 @@ def parse():
                    help='C4: pairs per packed chunk when a shard does not fit HBM')
     p.add_argument('--resident-gb', type=float, default=150.0,
                    help='C4: keep a shard\'s records resident up to this many GB')
+    p.add_argument('--stack', choices=('default', 'average'), default='default',
+                   help="layer stack: the default config.py:44-66 stack, or tuning.py:66-93's "
+                        "GCN-GCN-Average-NTN(16)")
     p.add_argument('--json-out', default='')
     p.add_argument('--emulate-world', type=int, default=0,
                    help='diagnostic: time rank 0\'s share of a W-GPU step on one GPU (no collective)')
@@ -106,6 +109,10 @@ def main():
     if c4:   # AIDS10k: N <= 30 needs Padding / NTN input_dim 30
         fl.update(layer_3='Padding:max_in_dims=30,padding_value=0',
                   layer_4='NTN:input_dim=30,feature_map_dim=10,inneract=relu,dropout=True,'
+                          'bias=True')
+    if args.stack == 'average':   # the tuning.py stack (layers_factory.py Average + NTN(16))
+        fl.update(num_layers=4, layer_2='Average',
+                  layer_3='NTN:input_dim=16,feature_map_dim=10,inneract=relu,dropout=True,'
                           'bias=True')
     if web:   # Web: N <= 512 needs Padding / NTN input_dim 512
         fl.update(layer_3='Padding:max_in_dims=512,padding_value=0',
@@ -188,7 +195,8 @@ def main():
     loss = float(model.loss_buf[0].item() + model.reg_buf[0].item())
 
     if rank == 0:
-        flops_pair = gs.flops_per_pair_web() if web else gs.flops_per_pair(D=D)
+        flops_pair = gs.flops_per_pair_web() if web else gs.flops_per_pair(
+            D=D, pool='average' if args.stack == 'average' else 'padding')
         bytes_pair = gs.csr_bytes_per_pair() if web else shard.record_bytes
         kern_pairs_s = shard.n / (kern_ms * 1e-3)
         achieved_tf = kern_pairs_s * flops_pair / 1e12
@@ -244,7 +252,9 @@ def main():
             'data': 'synthetic ({}-shaped graphs + GED labels, BASELINE.md §3)'.format(
                 'Web' if web else ('AIDS10knef' if c4 else 'AIDS700nef')),
             'config': {'workload': workload +
-                                   ', default 5-layer Siamese GCN-NTN, dropout {}'.format(args.dropout),
+                                   (', default 5-layer Siamese GCN-NTN' if args.stack == 'default' else
+                                    ', tuning.py GCN-GCN-Average-NTN(16) stack') +
+                                   ', dropout {}'.format(args.dropout),
                        'global_batch': total_pairs, 'n_max': gs.n_max, 'd_in': gs.d_in,
                        'kernel_path': _lib.PATH_NAMES[model.kernel_path],
                        'records': records,

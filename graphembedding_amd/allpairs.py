@@ -59,14 +59,18 @@ class GraphSet:
         per_graph = 4 * (n + 1) + 4 * n + 8 * (n + 2 * e)
         return float(2 * per_graph.mean() + 12)
 
-    def flops_per_pair(self, h1=32, h2=16, D=10, K=10) -> float:
+    def flops_per_pair(self, h1=32, h2=16, D=10, K=10, pool='padding') -> float:
         """Algorithmic FLOPs per pair, fwd+bwd (SURVEY §8(d) formula), averaged
-        over the all-pairs stream (every graph is g1 G times and g2 G times)."""
+        over the all-pairs stream (every graph is g1 G times and g2 G times).
+        pool='average': the tuning.py stack (no Dense; mean over nodes, NTN D = h2)."""
         n = np.array([g.number_of_nodes() for g in self.graphs], dtype=np.float64)
         e = np.array([g.number_of_edges() for g in self.graphs], dtype=np.float64)
         nnz = n + 2 * e
-        fwd = 2 * h1 * n + 2 * h1 * nnz + 2 * n * h1 * h2 + 2 * h2 * nnz + 2 * n * h2
-        bwd = (2 * h1 * nnz + 2 * h1 * n) + (2 * h2 * nnz + 4 * n * h1 * h2) + 4 * n * h2
+        head_f, head_b = (2 * n * h2, 4 * n * h2) if pool == 'padding' else (n * h2, n * h2)
+        if pool != 'padding':
+            D = h2
+        fwd = 2 * h1 * n + 2 * h1 * nnz + 2 * n * h1 * h2 + 2 * h2 * nnz + head_f
+        bwd = (2 * h1 * nnz + 2 * h1 * n) + (2 * h2 * nnz + 4 * n * h1 * h2) + head_b
         ntn_f = K * (4 * D + 2 * D * D + 2 * D)
         return float(2 * (fwd + bwd).mean() + 3 * ntn_f)
 

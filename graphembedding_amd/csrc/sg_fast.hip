@@ -3,6 +3,10 @@
 // identity) → Dense(16→1, relu) → Padding(D) → NTN(D, K=10, relu), every layer
 // with bias and dropout, Gaussian final act, broadcast or aligned MSE.
 //
+// AVG = true instantiates the tuning.py stack (tuning.py:66-93): GCN → GCN →
+// Average (layers.py:136-140) → NTN(16, K=10): the NTN input is the node mean of H2
+// (16 features) instead of the Dense/Padding node vector; the GCN part is shared.
+//
 // One wavefront owns one graph pair at a time.  The pair record is staged in
 // LDS; each graph instance is one 16-row MFMA tile whose rows are the nodes.
 // All seven GCN products (Â·Z0, D1·W1, Â·Z1 forward; Âᵀ·gH2, D1ᵀ·gZ1, gZ1·W1ᵀ,
@@ -54,6 +58,8 @@ struct FastArgs {
   const float *y_stats;
   float *s_out;
   float *slab;
+  float *ntn;     // AVG backward: [n_pairs][80] = x1|1 (32) | x2|1 (32) | gm (16), for the
+                  // NTN W/V/b gradients of sg_ntn_wgrad (sg_fast32.hip)
   uint32_t key;
   uint32_t thr0, thr1, thr2, thr4;
   float ik0, ik1, ik2, ik4;
@@ -64,29 +70,38 @@ struct FastArgs {
   int oW0, ob0, oW1, ob1, oWd, obd, oW, oV, oU, obn;
 };
 
-template <int D>
+template <int D, bool AVG = false>
 struct FastLds {
+  // NTN width DN (the Padding width D, or H2's 16 features after Average), the row
+  // stride WR of the NTN W tables and VS of the V table
+  static constexpr int DN = AVG ? FH2 : D, WR = AVG ? 16 : 12, VS = AVG ? 32 : 24;
   static constexpr int RW = 2 * D * D + 2 * D + 4;  // record words (multiple of 4)
   static constexpr int REC = 0;
   static constexpr int TILE = REC + RW;               // 2 x 16 x TS1 (D1 tiles)
-  static constexpr int X = TILE + 2 * 16 * TS1;       // x1[12] | x2[12] | spare; [47] = 0
-  static int wave_floats(int) { return X + 48; }
+  static constexpr int X = TILE + 2 * 16 * TS1;       // x1 | x2 (at 12, or 16 for AVG); [47] = 0
+  static constexpr int GE = X + 48;                   // AVG: ∂L/∂x1 | ∂L/∂x2 (16 each)
+  static int wave_floats(int) { return X + 48 + (AVG ? 32 : 0); }
   static int shared_floats(int d_in) {
-    return (d_in + 1) * FH1 + 2 * D * FK * 12 + FK * 24 + FH1 * W1S + FH2 * W1TS;
+    return (d_in + 1) * FH1 + 2 * DN * FK * WR + FK * VS + FH1 * W1S + FH2 * W1TS;
   }
 };
 
 
-// Flush slots of one lane: gW1 (8) | gW0/ik0 (16) | NTN dW (3 D) | dV (3 + 3) |
+// Flush slots of one lane: gW1 (8) | gW0/ik0 (16) | NTN dW (RN·DN) | dV (RN + RN) |
 // dbn, dU, loss | db0 (2), db1, dWd, dbd (pre-summed over row groups)
-template <int D>
+template <int D, bool AVG = false>
 struct FlushSlots {
-  static constexpr int NS = 8 + 16 + 3 * D + 6 + 3 + 5;
+  static constexpr int DN = FastLds<D, AVG>::DN, RN = (DN + 3) / 4;
+  // AVG: the NTN W, V and bias gradients go through the per-pair buffer instead
+  static constexpr int NWS = AVG ? 0 : RN * DN, NVS = AVG ? 0 : 2 * RN;
+  static constexpr int NS = 8 + 16 + NWS + NVS + 3 + 5;
 };
 
 // parameter index of slot s on lane l = 16 g + j, or -1 if the slot is padding
-template <int D>
+template <int D, bool AVG>
 __device__ __forceinline__ int fast_param(const FastArgs &A, int s, int l) {
+  constexpr int DN = FastLds<D, AVG>::DN, RN = (DN + 3) / 4;
+  constexpr int NWS = FlushSlots<D, AVG>::NWS, NVS = FlushSlots<D, AVG>::NVS;
   const int g = l >> 4, j = l & 15;
   if (s < 8) return A.oW1 + (16 * (s >> 2) + 4 * g + (s & 3)) * FH2 + j;
   s -= 8;
@@ -95,25 +110,25 @@ __device__ __forceinline__ int fast_param(const FastArgs &A, int s, int l) {
     return ty < A.d_in ? A.oW0 + ty * FH1 + 16 * ((s >> 2) & 1) + j : -1;
   }
   s -= 16;
-  if (s < 3 * D) {
-    const int a = 4 * (s / D) + g, b = s % D;
-    return (a < D && j < FK) ? A.oW + (a * D + b) * FK + j : -1;
+  if (s < NWS) {
+    const int a = 4 * (s / DN) + g, b = s % DN;
+    return (a < DN && j < FK) ? A.oW + (a * DN + b) * FK + j : -1;
   }
-  s -= 3 * D;
-  if (s < 6) {
-    const int a = 4 * (s % 3) + g;
-    return (a < D && j < FK) ? A.oV + j * 2 * D + (s >= 3 ? D : 0) + a : -1;
+  s -= NWS;
+  if (s < NVS) {
+    const int a = 4 * (s % RN) + g;
+    return (a < DN && j < FK) ? A.oV + j * 2 * DN + (s >= RN ? DN : 0) + a : -1;
   }
-  s -= 6;
+  s -= NVS;
   switch (s) {
-    case 0: return (g == 0 && j < FK) ? A.obn + j : -1;
+    case 0: return (!AVG && g == 0 && j < FK) ? A.obn + j : -1;
     case 1: return (g == 0 && j < FK) ? A.oU + j : -1;
     case 2: return l == 0 ? A.n_params : -1;
     case 3: return g == 0 ? A.ob0 + j : -1;
     case 4: return g == 0 ? A.ob0 + 16 + j : -1;
     case 5: return g == 0 ? A.ob1 + j : -1;
-    case 6: return g == 0 ? A.oWd + j : -1;
-    case 7: return l == 0 ? A.obd : -1;
+    case 6: return (!AVG && g == 0) ? A.oWd + j : -1;
+    case 7: return (!AVG && l == 0) ? A.obd : -1;
     default: return -1;
   }
 }
@@ -133,11 +148,14 @@ __device__ unsigned long long sg_fast_times[kTimeWaves * 5];
 #define SG_STAMP(slot, val) do {} while (0)
 #endif
 
-template <int D, bool BWD, bool ALIGNED, bool INTENDED>
+template <int D, bool BWD, bool ALIGNED, bool INTENDED, bool AVG>
 __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   SG_STAMP(0, __builtin_amdgcn_s_memrealtime());
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  using L = FastLds<D>;
+  using L = FastLds<D, AVG>;
+  constexpr int DN = L::DN, RN = (DN + 3) / 4, WR = L::WR, VS = L::VS;
+  constexpr int XO2 = AVG ? 16 : 12;       // x2 offset in the wave's x region
+  constexpr uint32_t NL = AVG ? 3u : 4u;   // layer index of the NTN (its dropout key)
   constexpr int RW4 = L::RW / 4;
   constexpr int NREC = (RW4 + 63) / 64;
   const int tid = threadIdx.x;
@@ -192,9 +210,9 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 
   float *sW0 = smem;                            // W0 · ik0, row d_in zero
   float *sWa = sW0 + (d_in + 1) * FH1;          // [a][k][12]: W[a][b][k] at b
-  float *sWb = sWa + D * FK * 12;               // [b][k][12]: W[a][b][k] at a
-  float *sV = sWb + D * FK * 12;                // [k][24]
-  float *sW1 = sV + FK * 24;                    // W1 · ik1 [32][16], row stride W1S (gD1)
+  float *sWb = sWa + DN * FK * WR;              // [b][k][WR]: W[a][b][k] at a
+  float *sV = sWb + DN * FK * WR;               // [k][VS]
+  float *sW1 = sV + FK * VS;                    // W1 · ik1 [32][16], row stride W1S (gD1)
   float *sW1T = sW1 + FH1 * W1S;                // W1ᵀ [16][32], row stride W1TS (Z1)
   float *W = smem + A.shared_floats + wv * A.wave_floats;
   float *sRec = W + L::REC;
@@ -229,14 +247,14 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   __syncthreads();
   for (int i = tid; i < (d_in + 1) * FH1; i += blockDim.x)
     sW0[i] = i < d_in * FH1 ? stg[A.oW0 + i] * A.ik0 : 0.f;
-  for (int i = tid; i < D * FK * 12; i += blockDim.x) {
-    const int x = i / (FK * 12), rem = i - x * FK * 12, k = rem / 12, y = rem - k * 12;
-    sWa[i] = y < D ? stg[A.oW + (x * D + y) * FK + k] : 0.f;
-    sWb[i] = y < D ? stg[A.oW + (y * D + x) * FK + k] : 0.f;
+  for (int i = tid; i < DN * FK * WR; i += blockDim.x) {
+    const int x = i / (FK * WR), rem = i - x * FK * WR, k = rem / WR, y = rem - k * WR;
+    sWa[i] = y < DN ? stg[A.oW + (x * DN + y) * FK + k] : 0.f;
+    sWb[i] = y < DN ? stg[A.oW + (y * DN + x) * FK + k] : 0.f;
   }
-  for (int i = tid; i < FK * 24; i += blockDim.x) {
-    const int k = i / 24, c = i - k * 24;
-    sV[i] = c < 2 * D ? stg[A.oV + k * 2 * D + c] : 0.f;
+  for (int i = tid; i < FK * VS; i += blockDim.x) {
+    const int k = i / VS, c = i - k * VS;
+    sV[i] = c < 2 * DN ? stg[A.oV + k * 2 * DN + c] : 0.f;
   }
   for (int i = tid; i < FH1 * FH2; i += blockDim.x) {
     const float w = stg[A.oW1 + i];
@@ -247,8 +265,8 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   const int j_ = tid & 15;
   const float b0v0 = stg[A.ob0 + j_], b0v1 = stg[A.ob0 + 16 + j_];
   const float b1v = stg[A.ob1 + j_];
-  const float wdv = stg[A.oWd + j_];
-  const float bd = stg[A.obd];
+  const float wdv = AVG ? 0.f : stg[A.oWd + j_];
+  const float bd = AVG ? 0.f : stg[A.obd];
   const bool kv = j_ < FK;
   const int kc = kv ? j_ : FK - 1;
   const float Uk = kv ? stg[A.oU + kc] : 0.f;
@@ -301,12 +319,14 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   f4 gw0[2][2] = {{f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}},
                   {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}}};
   float gb0a0 = 0.f, gb0a1 = 0.f, gb1a = 0.f, gwda = 0.f, gbda = 0.f;
-  float gWn[3][D];
+  constexpr int RW_ = AVG ? 1 : RN, DW_ = AVG ? 1 : DN;   // AVG: per-pair buffer instead
+  float gWn[RW_][DW_], gVa[RW_], gVb[RW_];
 #pragma unroll
-  for (int r = 0; r < 3; ++r)
+  for (int r = 0; r < RW_; ++r) {
+    gVa[r] = gVb[r] = 0.f;
 #pragma unroll
-    for (int b = 0; b < D; ++b) gWn[r][b] = 0.f;
-  float gVa[3] = {0.f, 0.f, 0.f}, gVb[3] = {0.f, 0.f, 0.f};
+    for (int b = 0; b < DW_; ++b) gWn[r][b] = 0.f;
+  }
   float gbn = 0.f, gUa = 0.f, lossa = 0.f;
   const float ybar = (BWD && !ALIGNED) ? A.y_stats[0] : 0.f;
 
@@ -386,18 +406,23 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
     // lanes 0..15: layer 0, node e = l; lanes 16..31: layer 4, element e = l - 16.
     // Node presence (e < N_side) is folded in (padded NTN inputs are 0).
     uint32_t km, km4;   // this lane's view: bit 16s + 4r ↔ node / element 4r + g of side s
+    uint32_t m4;        // bit 16s + e ↔ NTN-input element e of side s kept
     {
       const int e = l & 15;
       const bool hi = l >= 16;
-      const uint32_t h = sg_hash(pk, hi ? 4u : 0u, (uint32_t)e);
+      const uint32_t h = sg_hash(pk, hi ? NL : 0u, (uint32_t)e);
       const uint32_t thr = hi ? A.thr4 : A.thr0;
-      const uint64_t b0 = __ballot((l < 32) & (e < N0) & ((h & 0xFFFFu) < thr));
-      const uint64_t b1 = __ballot((l < 32) & (e < N1) & ((h >> 16) < thr));
+      // node presence folds into the node mask, and into the NTN mask when the NTN
+      // input is indexed by node (Padding); after Average it is indexed by feature
+      const bool p0 = (hi && AVG) || e < N0, p1 = (hi && AVG) || e < N1;
+      const uint64_t b0 = __ballot((l < 32) & p0 & ((h & 0xFFFFu) < thr));
+      const uint64_t b1 = __ballot((l < 32) & p1 & ((h >> 16) < thr));
       const uint32_t m0 = (uint32_t)(b0 & 0xFFFFu) | ((uint32_t)(b1 & 0xFFFFu) << 16);
-      const uint32_t m4 = (uint32_t)((b0 >> 16) & 0xFFFFu) | ((uint32_t)b1 & 0xFFFF0000u);
+      m4 = (uint32_t)((b0 >> 16) & 0xFFFFu) | ((uint32_t)b1 & 0xFFFF0000u);
       km = m0 >> g;
       km4 = m4 >> g;
     }
+    const float invn0 = N0 > 0 ? 1.f / (float)N0 : 0.f, invn1 = N1 > 0 ? 1.f / (float)N1 : 0.f;
 
     // Pair body for K0 / K1 node k-steps per side: a side with at most 8 nodes
     // has an all-zero third k-step (nodes 8..11), dropped from every
@@ -506,8 +531,29 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       // x = dropout(pad(relu(zpre))): row group g holds x_s[4r+g].  x > 0 exactly when
       // the node is present, zpre > 0 and the NTN-input element is kept: the backward
       // uses it as the whole mask of the Dense/Padding/dropout chain.
-      float xo[2][3], d2[2][3];
+      float xo[2][RN], d2[2][3];
       uint32_t kb = 0u;   // layer-2 keep bits, bit 3s + r
+      if constexpr (AVG) {
+        // x_s[j] = keep · mean over the side's nodes of H2[·][j] · ik4 (layers.py:136-140,
+        // 287-288): lane (g, j) holds the rows of nodes 4r + g; absent rows hold b1
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int KS = s2 ? K1 : K0, Ns = s2 ? N1 : N0;
+          float part = 0.f;
+#pragma unroll
+          for (int r = 0; r < KS; ++r) part += (4 * r + g < Ns) ? h2[s2][r] : 0.f;
+          const float e = xsum32(xsum16(part)) * (s2 ? invn1 : invn0);
+          const bool k4 = (m4 >> (16 * s2 + j)) & 1u;
+          if (g == 0) sX[XO2 * s2 + j] = k4 ? e * A.ik4 : 0.f;
+        }
+        sg_wsync();
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int r = 0; r < RN; ++r) xo[s2][r] = sX[XO2 * s2 + 4 * r + g];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) d2[0][r] = d2[1][r] = 0.f;
+      } else {
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         if (r < K0 || r < K1) {
@@ -541,30 +587,34 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         }
       }
       sg_wsync();
+      }   // !AVG
 
       // ================= NTN head (layers.py:282-310) =================
       // x_s is zero past 4 K_s elements: terms with a zero factor are dropped
       // (each is an exact fmaf(0, ·, acc) = acc)
-      constexpr int BL0 = 4 * K0 < D ? 4 * K0 : D, BL1 = 4 * K1 < D ? 4 * K1 : D;
-      float x2[D];
+      // (after Average every element can be nonzero: full width)
+      constexpr int BL0 = AVG ? DN : (4 * K0 < D ? 4 * K0 : D);
+      constexpr int BL1 = AVG ? DN : (4 * K1 < D ? 4 * K1 : D);
+      constexpr int RA = AVG ? RN : K0, RB = AVG ? RN : K1;   // row groups holding x_s
+      float x2[DN];
 #pragma unroll
-      for (int b = 0; b < BL1; ++b) x2[b] = sX[12 + b];
-      float u[3];
+      for (int b = 0; b < BL1; ++b) x2[b] = sX[XO2 + b];
+      float u[RN];
       float mpart = 0.f;
 #pragma unroll
-      for (int r = 0; r < 3; ++r) {
+      for (int r = 0; r < RN; ++r) {
         const int a = 4 * r + g;
-        const int ac = a < D ? a : 0;
-        if (r < K0) {
-          const float *wa = sWa + (ac * FK + kc) * 12;
+        const int ac = a < DN ? a : 0;
+        if (r < RA) {
+          const float *wa = sWa + (ac * FK + kc) * WR;
           float acc = 0.f;
 #pragma unroll
           for (int b = 0; b < BL1; ++b) acc = fmaf(wa[b], x2[b], acc);
           u[r] = acc;
           // x1[a] u[a][k] + V[k][a] x1[a] + V[k][D+a] x2[a]   (x of invalid a is 0)
-          mpart = fmaf(xo[0][r], acc + sV[kc * 24 + ac], mpart);
+          mpart = fmaf(xo[0][r], acc + sV[kc * VS + ac], mpart);
         }
-        if (r < K1) mpart = fmaf(xo[1][r], sV[kc * 24 + D + ac], mpart);
+        if (r < RB) mpart = fmaf(xo[1][r], sV[kc * VS + DN + ac], mpart);
       }
       const float m = xsum32(xsum16(mpart)) + bnk;
       const float rk = (kv & (m > 0.f)) ? m : 0.f;
@@ -590,34 +640,47 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       // ================= NTN backward =================
       const float gmk = (kv & (m > 0.f)) ? (INTENDED ? gs * Uk : gs * usum) : 0.f;
       if (g == 0) {
-        gbn += gmk;
+        if (!AVG) gbn += gmk;
         gUa += INTENDED ? gs * rk : gs * rsum;
       }
+      if constexpr (AVG) {
+        // this pair's row of the NTN-gradient buffer: x1|1 | x2|1 | gm (lane k = j of
+        // row group 0 holds gm_k)
+        float *nb_ = A.ntn + (size_t)(uint32_t)pcur * 80u;
+        if (l < 32) {
+          nb_[l] = l < DN ? sX[l] : (l == DN ? 1.f : 0.f);
+          nb_[32 + l] = l < DN ? sX[XO2 + l] : (l == DN ? 1.f : 0.f);
+        }
+        if (l < 16) nb_[64 + l] = l < FK ? gmk : 0.f;
+      }
       const float gmk4 = gmk * A.ik4;
-      float ge[2][3];   // dL/dx · ik4 (before the x > 0 mask)
+      float ge[2][RN];   // dL/dx · ik4 (before the x > 0 mask)
       {
-        float x1[D];
+        float x1[DN];
 #pragma unroll
         for (int a = 0; a < BL0; ++a) x1[a] = sX[a];
 #pragma unroll
-        for (int r = 0; r < 3; ++r) {
+        for (int r = 0; r < RN; ++r) {
           const int a = 4 * r + g;
-          const int ac = a < D ? a : 0;
-          if (r < K0) {
-            const float c = gmk * xo[0][r];
+          const int ac = a < DN ? a : 0;
+          ge[0][r] = ge[1][r] = 0.f;
+          if (r < RA) {
+            if constexpr (!AVG) {
+              const float c = gmk * xo[0][r];
 #pragma unroll
-            for (int b = 0; b < BL1; ++b) gWn[r][b] = fmaf(c, x2[b], gWn[r][b]);
-            gVa[r] = fmaf(gmk, xo[0][r], gVa[r]);
-            const float t1 = gmk4 * (sV[kc * 24 + ac] + u[r]);
+              for (int b = 0; b < BL1; ++b) gWn[r][b] = fmaf(c, x2[b], gWn[r][b]);
+              gVa[r] = fmaf(gmk, xo[0][r], gVa[r]);
+            }
+            const float t1 = gmk4 * (sV[kc * VS + ac] + u[r]);
             ge[0][r] = row_sum16(t1);
           }
-          if (r < K1) {
-            gVb[r] = fmaf(gmk, xo[1][r], gVb[r]);
-            const float *wb = sWb + (ac * FK + kc) * 12;
+          if (r < RB) {
+            if constexpr (!AVG) gVb[r] = fmaf(gmk, xo[1][r], gVb[r]);
+            const float *wb = sWb + (ac * FK + kc) * WR;
             float w = 0.f;
 #pragma unroll
             for (int aa = 0; aa < BL0; ++aa) w = fmaf(x1[aa], wb[aa], w);
-            const float t2 = gmk4 * (sV[kc * 24 + D + ac] + w);
+            const float t2 = gmk4 * (sV[kc * VS + DN + ac] + w);
             ge[1][r] = row_sum16(t2);
           }
         }
@@ -626,18 +689,39 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       // ================= GCN backward =================
       f4 gh2[2], gz1t[2];
       float dq[2][2][3];   // [side][t][q]: this lane's D1 entries
+      float gej[2] = {0.f, 0.f};   // AVG: ∂L/∂e_s[j] / N_s
+      if constexpr (AVG) {
+        // ∂L/∂x of element a = 4r + g (equal on a row's 16 lanes) → by feature j
+        float *sGE = W + L::GE;
+        if (j == 0) {
+#pragma unroll
+          for (int r = 0; r < RN; ++r) {
+            sGE[4 * r + g] = ge[0][r];
+            sGE[16 + 4 * r + g] = ge[1][r];
+          }
+        }
+        sg_wsync();
+        gej[0] = ((m4 >> j) & 1u) ? sGE[j] * invn0 : 0.f;
+        gej[1] = ((m4 >> (16 + j)) & 1u) ? sGE[16 + j] * invn1 : 0.f;
+      }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int KS = s ? K1 : K0;
         gh2[s] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int r = 0; r < KS; ++r) {
-          const float gp = xo[s][r] > 0.f ? ge[s][r] : 0.f;   // dropout4 · relu' · present
-          gwda = fmaf(d2[s][r], gp, gwda);
-          gbda += gp;   // equal on the 16 lanes of a row: lane j == 0 is flushed
-          const float v = ((kb >> (3 * s + r)) & 1u) ? gp * wdv * A.ik2 : 0.f;
-          gb1a += v;
-          gh2[s][r] = v;
+          if constexpr (AVG) {   // mean: every present node gets ∂L/∂e / N
+            const float v = (4 * r + g < (s ? N1 : N0)) ? gej[s] : 0.f;
+            gb1a += v;
+            gh2[s][r] = v;
+          } else {
+            const float gp = xo[s][r] > 0.f ? ge[s][r] : 0.f;   // dropout4 · relu' · present
+            gwda = fmaf(d2[s][r], gp, gwda);
+            gbda += gp;   // equal on the 16 lanes of a row: lane j == 0 is flushed
+            const float v = ((kb >> (3 * s + r)) & 1u) ? gp * wdv * A.ik2 : 0.f;
+            gb1a += v;
+            gh2[s][r] = v;
+          }
         }
         // gZ1 = Âᵀ gH2 in both orientations (Â symmetric, checked at pack time):
         //   gz1  rows = nodes (B of gW1 = D1ᵀ gZ1),  gz1t rows = j (A of gD1 = gZ1 W1ᵀ)
@@ -746,7 +830,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   // every parameter is hit exactly once, so the slab row is written directly.
   // Waves are summed in fixed order (deterministic).  The block owns the CU's
   // LDS (one block per CU), so all its waves' slots fit (fast_cfg).
-  constexpr int NS = FlushSlots<D>::NS;
+  constexpr int NS = FlushSlots<D, AVG>::NS;
   {
     // per-feature bias / Dense gradients: sum the four row groups in registers
     gb0a0 = xsum32(xsum16(gb0a0));
@@ -770,14 +854,16 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) Fw[64 * s++] = gw0[tau][t][r] * A.ik0;
+    if constexpr (!AVG) {
 #pragma unroll
-    for (int r = 0; r < 3; ++r)
+      for (int r = 0; r < RN; ++r)
 #pragma unroll
-      for (int b = 0; b < D; ++b) Fw[64 * s++] = gWn[r][b];
+        for (int b = 0; b < DN; ++b) Fw[64 * s++] = gWn[r][b];
 #pragma unroll
-    for (int r = 0; r < 3; ++r) Fw[64 * s++] = gVa[r];
+      for (int r = 0; r < RN; ++r) Fw[64 * s++] = gVa[r];
 #pragma unroll
-    for (int r = 0; r < 3; ++r) Fw[64 * s++] = gVb[r];
+      for (int r = 0; r < RN; ++r) Fw[64 * s++] = gVb[r];
+    }
     Fw[64 * s++] = gbn;
     Fw[64 * s++] = gUa;
     Fw[64 * s++] = lossa;
@@ -790,7 +876,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   __syncthreads();
   float *dst = A.slab + (size_t)blockIdx.x * (size_t)(A.n_params + 1);
   for (int idx = tid; idx < NS * 64; idx += blockDim.x) {
-    const int prm_i = fast_param<D>(A, idx >> 6, idx & 63);
+    const int prm_i = fast_param<D, AVG>(A, idx >> 6, idx & 63);
     if (prm_i < 0) continue;
     float acc = 0.f;
     for (int w = 0; w < nw; ++w) acc += F[(size_t)w * NS * 64 + idx];
@@ -807,12 +893,12 @@ struct FastCfg {
   int shared_floats, wave_floats;
 };
 
-template <int D>
+template <int D, bool AVG>
 FastCfg fast_cfg_t(int d_in, int n_params, int64_t n_pairs, bool bwd) {
   FastCfg c;
   c.D = D;
-  c.shared_floats = FastLds<D>::shared_floats(d_in);
-  c.wave_floats = FastLds<D>::wave_floats(d_in);
+  c.shared_floats = FastLds<D, AVG>::shared_floats(d_in);
+  c.wave_floats = FastLds<D, AVG>::wave_floats(d_in);
   // resident waves per CU allowed by registers: the backward kernel uses up to
   // 256 VGPRs (2 waves / SIMD), the forward-only one ~120 (4 waves / SIMD)
   const int wcap = bwd ? MAXW : 2 * MAXW;
@@ -824,7 +910,7 @@ FastCfg fast_cfg_t(int d_in, int n_params, int64_t n_pairs, bool bwd) {
     if (force > 0 && nw != force) continue;
     const size_t lds = (size_t)(c.shared_floats + nw * c.wave_floats) * 4u;
     if (lds > 163840u) break;
-    if (bwd && (size_t)nw * FlushSlots<D>::NS * 256u > 163840u) break;   // flush slots fit
+    if (bwd && (size_t)nw * FlushSlots<D, AVG>::NS * 256u > 163840u) break;   // flush slots fit
     int per_cu = (int)(163840u / lds);
     int res = per_cu * nw;
     if (res > wcap) res = wcap;  // register-limited occupancy
@@ -841,7 +927,7 @@ FastCfg fast_cfg_t(int d_in, int n_params, int64_t n_pairs, bool bwd) {
   if (per_cu > wcap / best) per_cu = wcap / best;
   if (per_cu < 1) per_cu = 1;
   // the flush dumps every wave's accumulator slots into the block's LDS
-  const size_t fl = bwd ? (size_t)best * FlushSlots<D>::NS * 64u * 4u : 0u;
+  const size_t fl = bwd ? (size_t)best * FlushSlots<D, AVG>::NS * 64u * 4u : 0u;
   // the prologue stages the parameter vector behind the shared tables
   const size_t stage = (size_t)(c.shared_floats + n_params) * 4u;
   const size_t need = fl > stage ? fl : stage;
@@ -858,7 +944,28 @@ FastCfg fast_cfg_t(int d_in, int n_params, int64_t n_pairs, bool bwd) {
 }  // namespace
 
 // --------------------------------------------------------------------------
+// tuning.py:66-93 stack: GCN(d_in→32, relu) → GCN(32→16) → Average → NTN(16, K=10)
+static bool fast_avg_shape(const sg_model_t *m, const SgGenPlan &P) {
+  if (m->num_layers != 4) return false;
+  const sg_layer_t *Ly = m->layers;
+  if (Ly[0].kind != SG_GCN || !Ly[0].sparse_inputs || Ly[0].output_dim != FH1 ||
+      Ly[0].act != SG_ACT_RELU || !Ly[0].bias)
+    return false;
+  if (Ly[1].kind != SG_GCN || Ly[1].input_dim != FH1 || Ly[1].output_dim != FH2 ||
+      Ly[1].act != SG_ACT_IDENTITY || !Ly[1].bias)
+    return false;
+  if (Ly[2].kind != SG_AVERAGE) return false;
+  if (Ly[3].kind != SG_NTN || Ly[3].input_dim != FH2 || Ly[3].output_dim != FK ||
+      Ly[3].act != SG_ACT_RELU || !Ly[3].bias)
+    return false;
+  if (m->n_max != 10 && m->n_max != 12) return false;
+  if (m->final_act != SG_FINAL_GAUSSIAN) return false;
+  if (m->d_in > 32) return false;
+  return P.n_params > 0;
+}
+
 static bool fast_shape(const sg_model_t *m, const SgGenPlan &P) {
+  if (fast_avg_shape(m, P)) return true;
   if (m->num_layers != 5) return false;
   const sg_layer_t *Ly = m->layers;
   if (Ly[0].kind != SG_GCN || !Ly[0].sparse_inputs || Ly[0].output_dim != FH1 ||
@@ -886,9 +993,14 @@ int sg_fast_supported(const sg_model_t *m, const SgGenPlan &P) {
   return fast_shape(m, P) ? 1 : 0;
 }
 
+static bool plan_avg(const SgGenPlan &P) { return P.nl == 3 && P.L[2].kind == SG_AVERAGE; }
+
 static FastCfg fast_cfg(const SgGenPlan &P, int64_t n_pairs, bool bwd) {
-  return P.n_max == 12 ? fast_cfg_t<12>(P.d_in, P.n_params, n_pairs, bwd)
-                       : fast_cfg_t<10>(P.d_in, P.n_params, n_pairs, bwd);
+  if (plan_avg(P))
+    return P.n_max == 12 ? fast_cfg_t<12, true>(P.d_in, P.n_params, n_pairs, bwd)
+                         : fast_cfg_t<10, true>(P.d_in, P.n_params, n_pairs, bwd);
+  return P.n_max == 12 ? fast_cfg_t<12, false>(P.d_in, P.n_params, n_pairs, bwd)
+                       : fast_cfg_t<10, false>(P.d_in, P.n_params, n_pairs, bwd);
 }
 
 int64_t sg_fast_slab_floats(const SgGenPlan &P, int64_t n_pairs) {
@@ -896,34 +1008,39 @@ int64_t sg_fast_slab_floats(const SgGenPlan &P, int64_t n_pairs) {
   return (int64_t)c.blocks * (P.n_params + 1);
 }
 
-template <int D, bool BWD, bool ALIGNED, bool INTENDED>
+template <int D, bool BWD, bool ALIGNED, bool INTENDED, bool AVG>
 static void launch_one(const FastCfg &c, const FastArgs &A, hipStream_t st) {
-  const void *fn = (const void *)sg_fast_kernel<D, BWD, ALIGNED, INTENDED>;
+  const void *fn = (const void *)sg_fast_kernel<D, BWD, ALIGNED, INTENDED, AVG>;
   if (c.lds > 65536u)
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds);
-  hipLaunchKernelGGL((sg_fast_kernel<D, BWD, ALIGNED, INTENDED>), dim3(c.blocks),
+  hipLaunchKernelGGL((sg_fast_kernel<D, BWD, ALIGNED, INTENDED, AVG>), dim3(c.blocks),
                      dim3(64 * c.waves), c.lds, st, A);
 }
 
-template <int D>
+template <int D, bool AVG>
 static void launch_fast(const FastCfg &c, bool bwd, bool aligned, bool intended,
                         const FastArgs &A, hipStream_t st) {
   if (!bwd) {
-    if (intended) launch_one<D, false, false, true>(c, A, st);
-    else launch_one<D, false, false, false>(c, A, st);
+    if (intended) launch_one<D, false, false, true, AVG>(c, A, st);
+    else launch_one<D, false, false, false, AVG>(c, A, st);
   } else if (aligned) {
-    if (intended) launch_one<D, true, true, true>(c, A, st);
-    else launch_one<D, true, true, false>(c, A, st);
+    if (intended) launch_one<D, true, true, true, AVG>(c, A, st);
+    else launch_one<D, true, true, false, AVG>(c, A, st);
   } else {
-    if (intended) launch_one<D, true, false, true>(c, A, st);
-    else launch_one<D, true, false, false>(c, A, st);
+    if (intended) launch_one<D, true, false, true, AVG>(c, A, st);
+    else launch_one<D, true, false, false, AVG>(c, A, st);
   }
 }
 
+int sg_ntn_wgrad_run(const float *ntn, int64_t n_pairs, int D, int oW, int oV, int obn, int C,
+                     float *slab, int blocks, hipStream_t st);
+
+int sg_fast_needs_ntn(const SgGenPlan &P) { return plan_avg(P) ? 1 : 0; }
+
 int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
                 const int32_t *order, int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
-                uint64_t seed, const float *y_stats, float *s_out, float *slab, int *blocks_out,
-                hipStream_t stream) {
+                uint64_t seed, const float *y_stats, float *s_out, float *slab, float *ntn,
+                int *blocks_out, hipStream_t stream) {
   const int D = P.n_max;
   FastCfg c = fast_cfg(P, n_pairs, bwd);
   // the kernel indexes pairs in 32 bits (2^31 records would be ≥ 1 TB)
@@ -939,10 +1056,13 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
   A.y_stats = y_stats;
   A.s_out = s_out;
   A.slab = slab;
+  A.ntn = ntn;
   A.key = sg_seed_key(seed);
   const float keep = m->keep_prob;
+  const bool avg = plan_avg(P);   // NTN is layer 3 after Average (no Dense / Padding)
   const float k0 = m->layers[0].dropout ? keep : 1.f, k1 = m->layers[1].dropout ? keep : 1.f;
-  const float k2 = m->layers[2].dropout ? keep : 1.f, k4 = m->layers[4].dropout ? keep : 1.f;
+  const float k2 = (!avg && m->layers[2].dropout) ? keep : 1.f;
+  const float k4 = m->layers[avg ? 3 : 4].dropout ? keep : 1.f;
   A.thr0 = sg_keep_threshold(k0);
   A.thr1 = sg_keep_threshold(k1);
   A.thr2 = sg_keep_threshold(k2);
@@ -961,16 +1081,27 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
   A.ob0 = P.L[0].offB;
   A.oW1 = P.L[1].offW;
   A.ob1 = P.L[1].offB;
-  A.oWd = P.L[2].offW;
-  A.obd = P.L[2].offB;
+  A.oWd = avg ? -1 : P.L[2].offW;
+  A.obd = avg ? -1 : P.L[2].offB;
   A.oW = P.offW;
   A.oV = P.offV;
   A.oU = P.offU;
   A.obn = P.offB;
   const bool aligned = m->loss_mode == SG_LOSS_ALIGNED;
   const bool intended = m->ntn_mode == SG_NTN_INTENDED;
-  if (D == 12) launch_fast<12>(c, bwd, aligned, intended, A, stream);
-  else launch_fast<10>(c, bwd, aligned, intended, A, stream);
+  if (avg) {
+    if (bwd && !ntn) return SG_ERR_ARG;
+    if (D == 12) launch_fast<12, true>(c, bwd, aligned, intended, A, stream);
+    else launch_fast<10, true>(c, bwd, aligned, intended, A, stream);
+    if (bwd) {
+      const int rc = sg_ntn_wgrad_run(ntn, n_pairs, FH2, P.offW, P.offV, P.offB, P.n_params + 1,
+                                      slab, c.blocks, stream);
+      if (rc != SG_OK) return rc;
+    }
+  } else {
+    if (D == 12) launch_fast<12, false>(c, bwd, aligned, intended, A, stream);
+    else launch_fast<10, false>(c, bwd, aligned, intended, A, stream);
+  }
   if (blocks_out) *blocks_out = c.blocks;
   return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
 }

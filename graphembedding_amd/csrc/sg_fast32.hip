@@ -820,6 +820,17 @@ int64_t sg_fast32_slab_floats(const SgGenPlan &P, int64_t n_pairs) {
 
 int64_t sg_fast32_ntn_floats(int64_t n_pairs) { return n_pairs * NBUF; }
 
+// NTN W / V / bias gradients from a per-pair buffer [n_pairs][80] (x1|1, x2|1 at
+// capacity 32, gm at 64) into the NTN columns of slab rows 0..blocks-1 (also used by
+// sg_fast's Average stack, D = 16)
+int sg_ntn_wgrad_run(const float *ntn, int64_t n_pairs, int D, int oW, int oV, int obn, int C,
+                     float *slab, int blocks, hipStream_t st) {
+  if (D < 1 || D > 31 || obn < 0) return SG_ERR_ARG;
+  hipLaunchKernelGGL(sg_ntn_wgrad_kernel, dim3(blocks), dim3(256), 0, st, ntn, n_pairs, D, oW, oV,
+                     obn, C, slab);
+  return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
+}
+
 int sg_fast32_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
                   const int32_t *order, int64_t n_pairs, int64_t pair_offset,
                   int64_t batch_total, const float *params, uint64_t seed, const float *y_stats,

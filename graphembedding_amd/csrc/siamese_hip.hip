@@ -32,10 +32,11 @@ int sg_generic_run(const SgGenPlan &P, bool bwd, const void *recs, const int32_t
 // fused fast path (sg_fast.hip)
 int sg_fast_supported(const sg_model_t *m, const SgGenPlan &P);
 int64_t sg_fast_slab_floats(const SgGenPlan &P, int64_t n_pairs);
+int sg_fast_needs_ntn(const SgGenPlan &P);
 int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
                 const int32_t *order, int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
-                uint64_t seed, const float *y_stats, float *s_out, float *slab, int *blocks_out,
-                hipStream_t stream);
+                uint64_t seed, const float *y_stats, float *s_out, float *slab, float *ntn,
+                int *blocks_out, hipStream_t stream);
 // fused capacity-32 path (sg_fast32.hip)
 int sg_fast32_supported(const sg_model_t *m, const SgGenPlan &P);
 // graph-store path for Web-sized graphs (sg_web.hip)
@@ -517,7 +518,8 @@ int64_t sg_workspace_bytes(const sg_model_t *model, int64_t n_pairs) {
   // room for either path (SG_DISABLE_FAST may route a fast-path model to the
   // generic kernel after the workspace was sized)
   int64_t bytes = ntn_offset_floats(c, n_pairs) * 4;
-  if (c.path == 2) bytes += sg_fast32_ntn_floats(n_pairs) * 4;
+  if (c.path == 2 || (c.path == 1 && sg_fast_needs_ntn(c.plan)))
+    bytes += sg_fast32_ntn_floats(n_pairs) * 4;   // per-pair NTN-gradient buffer
   bytes = (bytes + 255) & ~(int64_t)255;
   const int64_t label_bytes = (256 + 2) * 8;
   return (bytes > label_bytes ? bytes : label_bytes) + 256;
@@ -625,7 +627,7 @@ int32_t sg_forward_ex(const sg_model_t *model, const void *records, const int32_
   if (c.status != SG_OK) return c.status;
   if (c.path == 1)
     return sg_fast_run(model, c.plan, false, records, order, n_pairs, pair_offset, n_pairs, params,
-                       seed, nullptr, s_out, nullptr, nullptr, (hipStream_t)stream);
+                       seed, nullptr, s_out, nullptr, nullptr, nullptr, (hipStream_t)stream);
   if (c.path == 2)
     return sg_fast32_run(model, c.plan, false, records, order, n_pairs, pair_offset, n_pairs,
                          params, seed, nullptr, s_out, nullptr, nullptr, nullptr,
@@ -668,7 +670,8 @@ int32_t sg_fwd_bwd_ex(const sg_model_t *model, const void *records, const int32_
   int rc;
   if (c.path == 1)
     rc = sg_fast_run(model, c.plan, true, records, order, n_pairs, pair_offset, batch_total,
-                     params, seed, y_stats, s_out, slab, &nblk, st);
+                     params, seed, y_stats, s_out, slab, slab + ntn_offset_floats(c, n_pairs),
+                     &nblk, st);
   else if (c.path == 2)
     rc = sg_fast32_run(model, c.plan, true, records, order, n_pairs, pair_offset, batch_total,
                        params, seed, y_stats, s_out, slab, slab + ntn_offset_floats(c, n_pairs),

@@ -25,10 +25,11 @@ def _expected_order(prob, fused):
     return np.argsort(key, kind='stable').astype(np.int32)
 
 
-@pytest.mark.parametrize('name,fused', [('default', True), ('average', False),
-                                        ('default_bf16', True)])
+@pytest.mark.parametrize('name,fused', [('default', True), ('average', True),
+                                        ('attention', False), ('default_bf16', True)])
 def test_pair_order_is_stable_class_sort(gpu, name, fused):
-    ov = {'default': {}, 'average': AVERAGE_STACK, 'default_bf16': dict(record_dtype='bf16')}[name]
+    ov = {'default': {}, 'average': AVERAGE_STACK, 'default_bf16': dict(record_dtype='bf16'),
+          'attention': dict(AVERAGE_STACK, layer_2='Attention:input_dim=16')}[name]
     # > 2 sort chunks (8192 records), ragged last chunk, 1..10-node graphs
     prob = small_problem(n_graphs=50, n_pairs=20011, seed=31, n_lo=1, n_hi=10,
                          flags_overrides=ov)

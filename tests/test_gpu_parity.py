@@ -140,12 +140,15 @@ def test_nmax30_aids10k_shape(gpu):
     _check_grad(model.grad.cpu().numpy(), ref.grad_mse)
 
 
-def test_fast_path_matches_generic_path(gpu, monkeypatch):
-    """The fused MFMA kernel and the generic LDS kernel agree on the default
-    stack (dropout on) — the generic path is the on-GPU cross-check."""
-    prob = small_problem(n_graphs=40, n_pairs=2000, seed=17)
+@pytest.mark.parametrize('stack', ['default', 'average'])
+def test_fast_path_matches_generic_path(gpu, monkeypatch, stack):
+    """The fused MFMA kernel and the generic LDS kernel agree on the default and
+    the tuning.py Average stacks (dropout on) — the generic path is the on-GPU
+    cross-check."""
+    prob = small_problem(n_graphs=40, n_pairs=2000, seed=17,
+                         flags_overrides=AVERAGE_STACK if stack == 'average' else None)
     model, batch = prob.make_gpu_model(device=gpu)
-    assert model.kernel_path == 1, 'default stack must take the fused path'
+    assert model.kernel_path == 1, 'the stack must take the fused path'
     seed = 99
     s_fast = model.pred_sim_without_act(batch, seed=seed).cpu().numpy()
     model.fwd_bwd(batch, seed=seed)
