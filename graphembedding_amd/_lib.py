@@ -116,6 +116,11 @@ def lib():
     L.sg_adam_workspace_bytes.restype = c_i64
     L.sg_adam_tf_ex.argtypes = [vp, vp, vp, vp, c_i64, c_f, c_f, c_f, c_f, c_f, vp, vp, vp, vp]
     L.sg_adam_tf_ex.restype = c_i32
+    L.sg_fwd_bwd_dseed.argtypes = [pm, vp, vp, c_i64, c_i64, c_i64, vp, vp, vp, c_i32, vp, vp,
+                                   vp, vp, vp]
+    L.sg_fwd_bwd_dseed.restype = c_i32
+    L.sg_seed_advance.argtypes = [vp, c_u64, vp]
+    L.sg_seed_advance.restype = c_i32
     pc = ctypes.POINTER(SgCsrStore)
     L.sg_web_workspace_bytes.argtypes = [pm, c_i64]
     L.sg_web_workspace_bytes.restype = c_i64
@@ -137,7 +142,7 @@ EXPORTED_SYMBOLS = ('sg_version', 'sg_record_bytes', 'sg_record_bytes_ex', 'sg_m
                     'sg_forward_ex', 'sg_fwd_bwd_ex', 'sg_pair_order',
                     'sg_pair_order_workspace_bytes', 'sg_sampler_random', 'sg_sampler_density',
                     'sg_adam_workspace_bytes', 'sg_adam_tf_ex', 'sg_web_workspace_bytes',
-                    'sg_web_forward', 'sg_web_fwd_bwd')
+                    'sg_web_forward', 'sg_web_fwd_bwd', 'sg_fwd_bwd_dseed', 'sg_seed_advance')
 
 # sg_dtype: storage type of Â in the pair records
 DTYPES = {'f32': 0, 'bf16': 1}
@@ -289,6 +294,22 @@ def fwd_bwd(m: SgModel, records, n_pairs, pair_offset, batch_total, params, seed
                               int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(y_stats), int(add_label_term),
                               _ptr(s_out), _ptr(grad_out), _ptr(loss_out), _ptr(workspace),
                               _stream(stream)), 'sg_fwd_bwd_ex')
+
+
+def fwd_bwd_dseed(m: SgModel, records, n_pairs, pair_offset, batch_total, params, seed_dev,
+                  y_stats, add_label_term, s_out, grad_out, loss_out, workspace, stream=None,
+                  order=None):
+    """fwd_bwd with the dropout seed read from the device (int64 tensor [1])."""
+    check(lib().sg_fwd_bwd_dseed(ctypes.byref(m), _ptr(records), _ptr(order), int(n_pairs),
+                                 int(pair_offset), int(batch_total), _ptr(params), _ptr(seed_dev),
+                                 _ptr(y_stats), int(add_label_term), _ptr(s_out), _ptr(grad_out),
+                                 _ptr(loss_out), _ptr(workspace), _stream(stream)),
+          'sg_fwd_bwd_dseed')
+
+
+def seed_advance(seed_dev, delta=1, stream=None):
+    check(lib().sg_seed_advance(_ptr(seed_dev), int(delta) & 0xFFFFFFFFFFFFFFFF,
+                                _stream(stream)), 'sg_seed_advance')
 
 
 def sampler_random(state, sigma, n, count, pairs_out, stream=None):

@@ -61,6 +61,8 @@ struct FastArgs {
   float *ntn;     // AVG backward: [n_pairs][80] = x1|1 (32) | x2|1 (32) | gm (16), for the
                   // NTN W/V/b gradients of sg_ntn_wgrad (sg_fast32.hip)
   uint32_t key;
+  const uint64_t *seed_dev;   // non-null: the dropout seed is read from device memory
+                              // (graph-captured steps, sg_fwd_bwd_dseed)
   uint32_t thr0, thr1, thr2, thr4;
   float ik0, ik1, ik2, ik4;
   float yeta;
@@ -168,6 +170,11 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   const uint32_t lb2 = (uint32_t)(FH2 * g + j);   // layer 2: e = 16 n + j
   const int d_in = A.d_in;
   const float *__restrict__ prm = A.params;
+  uint32_t key = A.key;   // sg_seed_key of the dropout seed
+  if (A.seed_dev) {
+    const uint64_t sd = *A.seed_dev;
+    key = ((uint32_t)sd * 0x85EBCA6Bu) ^ (uint32_t)(sd >> 32);
+  }
 
   // ---- pair schedule; the first record is loaded during the prologue ----
   // Slots are handed out round by round (round r: slots [r·S, r·S + S), S = all
@@ -400,7 +407,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
     int N1 = __builtin_amdgcn_readfirstlane(((const int *)sRec)[2 * D * D + 2 * D + 1]);
     N0 = N0 < 0 ? 0 : (N0 > D ? D : N0);
     N1 = N1 < 0 ? 0 : (N1 > D ? D : N1);
-    const uint32_t pk = sg_pair_key(A.key, (uint32_t)(A.pair_offset + pcur));
+    const uint32_t pk = sg_pair_key(key, (uint32_t)(A.pair_offset + pcur));
 
     // ---- layer-0 (node) and NTN-input dropout masks: one hash per lane, two ballots ----
     // lanes 0..15: layer 0, node e = l; lanes 16..31: layer 4, element e = l - 16.
@@ -1040,7 +1047,7 @@ int sg_fast_needs_ntn(const SgGenPlan &P) { return plan_avg(P) ? 1 : 0; }
 int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
                 const int32_t *order, int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
                 uint64_t seed, const float *y_stats, float *s_out, float *slab, float *ntn,
-                int *blocks_out, hipStream_t stream) {
+                int *blocks_out, hipStream_t stream, const uint64_t *seed_dev) {
   const int D = P.n_max;
   FastCfg c = fast_cfg(P, n_pairs, bwd);
   // the kernel indexes pairs in 32 bits (2^31 records would be ≥ 1 TB)
@@ -1058,6 +1065,7 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
   A.slab = slab;
   A.ntn = ntn;
   A.key = sg_seed_key(seed);
+  A.seed_dev = seed_dev;
   const float keep = m->keep_prob;
   const bool avg = plan_avg(P);   // NTN is layer 3 after Average (no Dense / Padding)
   const float k0 = m->layers[0].dropout ? keep : 1.f, k1 = m->layers[1].dropout ? keep : 1.f;

@@ -36,7 +36,7 @@ int sg_fast_needs_ntn(const SgGenPlan &P);
 int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
                 const int32_t *order, int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
                 uint64_t seed, const float *y_stats, float *s_out, float *slab, float *ntn,
-                int *blocks_out, hipStream_t stream);
+                int *blocks_out, hipStream_t stream, const uint64_t *seed_dev = nullptr);
 // fused capacity-32 path (sg_fast32.hip)
 int sg_fast32_supported(const sg_model_t *m, const SgGenPlan &P);
 // graph-store path for Web-sized graphs (sg_web.hip)
@@ -644,16 +644,18 @@ int32_t sg_fwd_bwd(const sg_model_t *model, const void *records, int64_t n_pairs
                        y_stats, add_label_term, s_out, grad_out, loss_out, workspace, stream);
 }
 
-int32_t sg_fwd_bwd_ex(const sg_model_t *model, const void *records, const int32_t *order,
-                      int64_t n_pairs, int64_t pair_offset, int64_t batch_total,
-                      const float *params, uint64_t seed, const float *y_stats,
-                      int32_t add_label_term, float *s_out, float *grad_out, float *loss_out,
-                      void *workspace, sg_stream_t stream) {
+static int32_t fwd_bwd_impl(const sg_model_t *model, const void *records, const int32_t *order,
+                            int64_t n_pairs, int64_t pair_offset, int64_t batch_total,
+                            const float *params, uint64_t seed, const uint64_t *seed_dev,
+                            const float *y_stats, int32_t add_label_term, float *s_out,
+                            float *grad_out, float *loss_out, void *workspace,
+                            sg_stream_t stream) {
   if (n_pairs < 0 || pair_offset < 0) return SG_ERR_ARG;
   if (order && n_pairs > 0x7FFFFFFF) return SG_ERR_ARG;
   if (!params || !grad_out || !workspace) return SG_ERR_ARG;
   PathChoice c = choose_path(model, true);
   if (c.status != SG_OK) return c.status;
+  if (seed_dev && c.path != 1) return SG_ERR_UNSUPPORTED;   // device seed: fused path only
   if (model->loss_mode == SG_LOSS_BROADCAST && !y_stats) return SG_ERR_ARG;
   if (model->loss_mode == SG_LOSS_ALIGNED && batch_total <= 0) return SG_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
@@ -671,7 +673,7 @@ int32_t sg_fwd_bwd_ex(const sg_model_t *model, const void *records, const int32_
   if (c.path == 1)
     rc = sg_fast_run(model, c.plan, true, records, order, n_pairs, pair_offset, batch_total,
                      params, seed, y_stats, s_out, slab, slab + ntn_offset_floats(c, n_pairs),
-                     &nblk, st);
+                     &nblk, st, seed_dev);
   else if (c.path == 2)
     rc = sg_fast32_run(model, c.plan, true, records, order, n_pairs, pair_offset, batch_total,
                        params, seed, y_stats, s_out, slab, slab + ntn_offset_floats(c, n_pairs),
@@ -683,6 +685,38 @@ int32_t sg_fwd_bwd_ex(const sg_model_t *model, const void *records, const int32_
   float *part = slab + (size_t)nblk * C;
   return launch_reduce(slab, nblk, C, part, grad_out, loss_out, y_stats,
                        model->loss_mode == SG_LOSS_BROADCAST ? add_label_term : 0, st);
+}
+
+int32_t sg_fwd_bwd_ex(const sg_model_t *model, const void *records, const int32_t *order,
+                      int64_t n_pairs, int64_t pair_offset, int64_t batch_total,
+                      const float *params, uint64_t seed, const float *y_stats,
+                      int32_t add_label_term, float *s_out, float *grad_out, float *loss_out,
+                      void *workspace, sg_stream_t stream) {
+  return fwd_bwd_impl(model, records, order, n_pairs, pair_offset, batch_total, params, seed,
+                      nullptr, y_stats, add_label_term, s_out, grad_out, loss_out, workspace,
+                      stream);
+}
+
+int32_t sg_fwd_bwd_dseed(const sg_model_t *model, const void *records, const int32_t *order,
+                         int64_t n_pairs, int64_t pair_offset, int64_t batch_total,
+                         const float *params, const uint64_t *seed_dev, const float *y_stats,
+                         int32_t add_label_term, float *s_out, float *grad_out, float *loss_out,
+                         void *workspace, sg_stream_t stream) {
+  if (!seed_dev) return SG_ERR_ARG;
+  return fwd_bwd_impl(model, records, order, n_pairs, pair_offset, batch_total, params, 0,
+                      seed_dev, y_stats, add_label_term, s_out, grad_out, loss_out, workspace,
+                      stream);
+}
+
+__global__ void sg_seed_add_kernel(uint64_t *seed, uint64_t delta) {
+  if (threadIdx.x == 0) seed[0] += delta;
+}
+
+int32_t sg_seed_advance(uint64_t *seed_dev, uint64_t delta, sg_stream_t stream) {
+  if (!seed_dev) return SG_ERR_ARG;
+  hipLaunchKernelGGL(sg_seed_add_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, seed_dev,
+                     delta);
+  return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
 }
 
 int32_t sg_adam_tf(float *params, float *m, float *v, const float *grad, int64_t n, float lr,

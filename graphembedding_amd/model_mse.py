@@ -336,6 +336,15 @@ class SiameseGCNTNMSE(object):
             return None
         return float(self.loss_buf[0].item() + self.reg_buf[0].item())
 
+    def capture_train_steps(self, feed, n_steps: int = 1):
+        """A hipGraph of n_steps reference train steps (train.py:8-44: get_feed_dict
+        then sess.run([opt_op, loss]) with B = 5 pairs): DeviceFeed.next_batch →
+        sg_fwd_bwd_dseed → ApplyAdam → seed + 1, all stream-ordered with no host sync.
+        The dropout seed lives on the device, so every replay draws the masks an eager
+        step with the same step_count would.  Returns a GraphSteps whose replay() runs
+        the captured steps; fused path (default / Average stack) only."""
+        return GraphSteps(self, feed, n_steps)
+
     def val_loss(self, batch: Batch, seed=None):
         self.fwd_bwd(batch, seed)
         reg = self.flags.weight_decay * 0.5 * float((self.params.double() ** 2).sum().item())
@@ -368,6 +377,60 @@ class SiameseGCNTNMSE(object):
 
     def load(self, path):
         self.load_state_dict(self.torch.load(path, weights_only=True))
+
+
+class GraphSteps(object):
+    """Captured train steps of SiameseGCNTNMSE (see capture_train_steps)."""
+
+    def __init__(self, model, feed, n_steps: int = 1):
+        import torch
+        if model.kernel_path != 1:
+            raise RuntimeError('graph-captured steps need the fused path (kernel path 1)')
+        self.model, self.feed, self.n_steps = model, feed, int(n_steps)
+        m = model
+        self.seed_dev = torch.tensor([m._seed(None)], dtype=torch.int64, device=m.device)
+        ws = m.workspace(feed.B)
+        state = self._snapshot()
+        # warm-up on a side stream (allocator pools, lazy handles), then restore
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self._body(ws)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self._restore(state)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            for _ in range(self.n_steps):
+                self._body(ws)
+        torch.cuda.synchronize()
+        self._restore(state)   # capture records the work; the state must not move
+
+    def _body(self, ws):
+        m = self.model
+        b = self.feed.next_batch()
+        _lib.fwd_bwd_dseed(m.sg, b.records, b.n_pairs, b.pair_offset, b.batch_total, m.params,
+                           self.seed_dev, b.y_stats, 1, None, m.grad, m.loss_buf, ws)
+        m.apply_adam()
+        _lib.seed_advance(self.seed_dev, 1)
+
+    def _snapshot(self):
+        m, f = self.model, self.feed
+        return [t.clone() for t in (m.params, m.adam_m, m.adam_v, m.beta_powers,
+                                    f.sampler.state, self.seed_dev)]
+
+    def _restore(self, st):
+        m, f = self.model, self.feed
+        for dst, src in zip((m.params, m.adam_m, m.adam_v, m.beta_powers, f.sampler.state,
+                             self.seed_dev), st):
+            dst.copy_(src)
+
+    def replay(self, times: int = 1):
+        """Run the captured steps `times` times; leaves the last step's loss_mse in
+        model.loss_buf and advances model.step_count like eager steps."""
+        for _ in range(int(times)):
+            self.graph.replay()
+        self.model.step_count += self.n_steps * int(times)
 
 
 def create_model(model, input_dim, flags=None, **kw):

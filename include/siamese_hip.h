@@ -229,6 +229,21 @@ int32_t sg_fwd_bwd_ex(const sg_model_t *model, const void *records, const int32_
                       void *workspace, sg_stream_t stream);
 
 /*
+ * Graph-captured training steps (library 1.5).  sg_fwd_bwd_ex with the dropout seed
+ * read from device memory at kernel time, so one hipGraph capture of a step
+ * (feed → fwd_bwd → Adam → sg_seed_advance) replays with a new seed each time: the
+ * reference's train loop (train.py:8-44, B = 5 pairs per sess.run) is launch-bound.
+ * Fused path (sg_model_validate path 1) only; other models give SG_ERR_UNSUPPORTED.
+ * sg_seed_advance adds delta to *seed_dev on the stream.
+ */
+int32_t sg_fwd_bwd_dseed(const sg_model_t *model, const void *records, const int32_t *order,
+                         int64_t n_pairs, int64_t pair_offset, int64_t batch_total,
+                         const float *params, const uint64_t *seed_dev, const float *y_stats,
+                         int32_t add_label_term, float *s_out, float *grad_out, float *loss_out,
+                         void *workspace, sg_stream_t stream);
+int32_t sg_seed_advance(uint64_t *seed_dev, uint64_t delta, sg_stream_t stream);
+
+/*
  * Device-side pair samplers (library 1.4; samplers.py:19-68).  The reference's
  * samplers draw only from fresh random.Random(seed) generators with known seeds,
  * so the host builds their tables once with CPython's `random`; these calls then

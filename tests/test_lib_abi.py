@@ -55,7 +55,10 @@ def test_validate_paths_and_param_counts(L):
     assert path2 == 1 and n2 == n
     avg = small_problem(flags_overrides=AVERAGE_STACK)
     n3, path3 = _lib.validate(_model(avg))
-    assert path3 == 0 and n3 == avg.params.size           # generic kernel
+    assert path3 == 1 and n3 == avg.params.size           # tuning.py stack → fused (AVG)
+    att = small_problem(flags_overrides=dict(AVERAGE_STACK, layer_2='Attention:input_dim=16'))
+    n4, path4 = _lib.validate(_model(att))
+    assert path4 == 0 and n4 == att.params.size           # generic kernel
     assert _lib.workspace_bytes(_model(prob), 490000) > 0
 
 
