@@ -189,6 +189,16 @@ def main():
 
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     total_pairs = shard.total
+    # the eval path (train.py:47-74 test matrix; pred_sim_without_act): forward only over
+    # the same resident batch, one launch per pass (reported beside the training metric)
+    fwd_rate = None
+    if world == 1 and batch is not None and not ew:
+        torch.cuda.synchronize()
+        f0 = time.perf_counter()
+        for _ in range(5):
+            model.pred_sim_without_act(batch)
+        torch.cuda.synchronize()
+        fwd_rate = 5 * batch.n_pairs / (time.perf_counter() - f0)
     value = total_pairs * args.steps / elapsed
     if ew:
         value = shard.n * args.steps / elapsed   # diagnostic: one emulated rank's own rate
@@ -274,6 +284,7 @@ def main():
                              'frac': achieved_gbs / HBM_PEAK_GBS,
                              'bytes_per_pair': bytes_pair},
             'cpu_baseline': cpu,
+            'forward_pairs_per_s': fwd_rate,
             'loss': loss,
         }
         line = json.dumps(out)
