@@ -51,6 +51,18 @@ class SgCsrStore(ctypes.Structure):
                 ('max_nnz', ctypes.c_int32)]
 
 
+class SgFeed(ctypes.Structure):
+    """sg_feed_t: host struct of device pointers (one step's get_feed_dict)."""
+    _fields_ = [('kind', ctypes.c_int32), ('state', ctypes.c_void_p), ('sigma', ctypes.c_void_p),
+                ('n', ctypes.c_int32), ('dens_order', ctypes.c_void_p), ('bins', ctypes.c_void_p),
+                ('item_table', ctypes.c_void_p), ('n_bins', ctypes.c_int32),
+                ('bin_size', ctypes.c_int32), ('batch', ctypes.c_int32), ('compat', ctypes.c_int32),
+                ('label_matrix', ctypes.c_void_p), ('label_n', ctypes.c_int32),
+                ('store_adj', ctypes.c_void_p), ('store_types', ctypes.c_void_p),
+                ('store_n', ctypes.c_void_p), ('n_graphs', ctypes.c_int32),
+                ('n_max', ctypes.c_int32), ('adj_dtype', ctypes.c_int32)]
+
+
 class SiameseHipError(RuntimeError):
     pass
 
@@ -121,6 +133,8 @@ def lib():
     L.sg_fwd_bwd_dseed.restype = c_i32
     L.sg_seed_advance.argtypes = [vp, c_u64, vp]
     L.sg_seed_advance.restype = c_i32
+    L.sg_feed_step.argtypes = [ctypes.POINTER(SgFeed), vp, vp, vp, vp, vp, vp]
+    L.sg_feed_step.restype = c_i32
     pc = ctypes.POINTER(SgCsrStore)
     L.sg_web_workspace_bytes.argtypes = [pm, c_i64]
     L.sg_web_workspace_bytes.restype = c_i64
@@ -142,7 +156,8 @@ EXPORTED_SYMBOLS = ('sg_version', 'sg_record_bytes', 'sg_record_bytes_ex', 'sg_m
                     'sg_forward_ex', 'sg_fwd_bwd_ex', 'sg_pair_order',
                     'sg_pair_order_workspace_bytes', 'sg_sampler_random', 'sg_sampler_density',
                     'sg_adam_workspace_bytes', 'sg_adam_tf_ex', 'sg_web_workspace_bytes',
-                    'sg_web_forward', 'sg_web_fwd_bwd', 'sg_fwd_bwd_dseed', 'sg_seed_advance')
+                    'sg_web_forward', 'sg_web_fwd_bwd', 'sg_fwd_bwd_dseed', 'sg_seed_advance',
+                    'sg_feed_step')
 
 # sg_dtype: storage type of Â in the pair records
 DTYPES = {'f32': 0, 'bf16': 1}
@@ -310,6 +325,13 @@ def fwd_bwd_dseed(m: SgModel, records, n_pairs, pair_offset, batch_total, params
 def seed_advance(seed_dev, delta=1, stream=None):
     check(lib().sg_seed_advance(_ptr(seed_dev), int(delta) & 0xFFFFFFFFFFFFFFFF,
                                 _stream(stream)), 'sg_seed_advance')
+
+
+def feed_step(feed: SgFeed, pairs_out, records, labels_out, y_stats_out, status_out=None,
+              stream=None):
+    check(lib().sg_feed_step(ctypes.byref(feed), _ptr(pairs_out), _ptr(records),
+                             _ptr(labels_out), _ptr(y_stats_out), _ptr(status_out),
+                             _stream(stream)), 'sg_feed_step')
 
 
 def sampler_random(state, sigma, n, count, pairs_out, stream=None):

@@ -148,3 +148,46 @@ __host__ __device__ __forceinline__ uint32_t sg_f32_to_bf16(float f) {
   __builtin_memcpy(&u, &f, 4);
   return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
 }
+
+// One pair record (layout in siamese_hip.h) gathered from a dense-slot graph store by
+// one wavefront (lane = 0..63): store Â [G][nmax][nmax] f32, types [G][nmax], n [G].
+// Invalid graph ids write a zero record and SG_ERR_ARG into *status.
+__device__ __forceinline__ void sg_pack_record(const float *__restrict__ sadj,
+                                               const int32_t *__restrict__ stypes,
+                                               const int32_t *__restrict__ sn, int n_graphs,
+                                               int nmax, int bf16, int g0, int g1, float label,
+                                               int64_t tag, uint32_t *__restrict__ dst,
+                                               int rec_words, int lane,
+                                               int32_t *__restrict__ status) {
+  const bool bad = g0 < 0 || g0 >= n_graphs || g1 < 0 || g1 >= n_graphs;
+  if (bad && lane == 0 && status) atomicExch(status, (int32_t)SG_ERR_ARG);
+  const int nn = nmax * nmax;
+  const int aw = bf16 ? nn : 2 * nn;               // adjacency words
+  const int tail = 2 * nmax + 4;                    // types, n_nodes, label, tag
+  auto adj_at = [&](int e) -> float {               // e in [0, 2 nn): side e / nn
+    const int s = e / nn, o = e - s * nn;
+    return sadj[(size_t)(s ? g1 : g0) * nn + o];
+  };
+  for (int w = lane; w < rec_words; w += SG_WAVE) {
+    uint32_t v = 0u;
+    if (!bad) {
+      if (w < aw) {
+        v = bf16 ? (sg_f32_to_bf16(adj_at(2 * w)) | (sg_f32_to_bf16(adj_at(2 * w + 1)) << 16))
+                 : __float_as_uint(adj_at(w));
+      } else if (w < aw + tail) {
+        const int o = w - aw;
+        if (o < 2 * nmax) {
+          const int s = o / nmax, i = o - s * nmax;
+          v = (uint32_t)stypes[(size_t)(s ? g1 : g0) * nmax + i];
+        } else if (o < 2 * nmax + 2) {
+          v = (uint32_t)sn[(o == 2 * nmax) ? g0 : g1];
+        } else if (o == 2 * nmax + 2) {
+          v = __float_as_uint(label);
+        } else {
+          v = (uint32_t)(tag & 0x7FFFFFFF);
+        }
+      }
+    }
+    dst[w] = v;
+  }
+}

@@ -189,39 +189,9 @@ __global__ void __launch_bounds__(256) sg_pack_kernel(const float *__restrict__ 
   const int lane = threadIdx.x & 63;
   const int64_t p = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (p >= n) return;
-  const int g0 = pidx[2 * p], g1 = pidx[2 * p + 1];
-  const bool bad = g0 < 0 || g0 >= n_graphs || g1 < 0 || g1 >= n_graphs;
-  if (bad && lane == 0 && status) atomicExch(status, (int32_t)SG_ERR_ARG);
-  const int nn = nmax * nmax;
-  const int aw = bf16 ? nn : 2 * nn;               // adjacency words
-  const int tail = 2 * nmax + 4;                    // types, n_nodes, label, tag
-  uint32_t *dst = recs + (size_t)p * rec_words;
-  auto adj_at = [&](int e) -> float {               // e in [0, 2 nn): side e / nn
-    const int s = e / nn, o = e - s * nn;
-    return sadj[(size_t)(s ? g1 : g0) * nn + o];
-  };
-  for (int w = lane; w < rec_words; w += SG_WAVE) {
-    uint32_t v = 0u;
-    if (!bad) {
-      if (w < aw) {
-        v = bf16 ? (sg_f32_to_bf16(adj_at(2 * w)) | (sg_f32_to_bf16(adj_at(2 * w + 1)) << 16))
-                 : __float_as_uint(adj_at(w));
-      } else if (w < aw + tail) {
-        const int o = w - aw;
-        if (o < 2 * nmax) {
-          const int s = o / nmax, i = o - s * nmax;
-          v = (uint32_t)stypes[(size_t)(s ? g1 : g0) * nmax + i];
-        } else if (o < 2 * nmax + 2) {
-          v = (uint32_t)sn[(o == 2 * nmax) ? g0 : g1];
-        } else if (o == 2 * nmax + 2) {
-          v = __float_as_uint(labels ? labels[p] : 0.f);
-        } else {
-          v = (uint32_t)(p & 0x7FFFFFFF);
-        }
-      }
-    }
-    dst[w] = v;
-  }
+  sg_pack_record(sadj, stypes, sn, n_graphs, nmax, bf16, pidx[2 * p], pidx[2 * p + 1],
+                 labels ? labels[p] : 0.f, p, recs + (size_t)p * rec_words, rec_words, lane,
+                 status);
 }
 
 // ---- processing order: stable counting sort of the records by cost class ----

@@ -159,19 +159,33 @@ class DeviceFeed(object):
         self.records = torch.empty(B * record_words(model.n_max, model.record_dtype),
                                    dtype=torch.int32, device=dev)
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.labels = torch.empty(B, dtype=torch.float32, device=dev)
+        self.y_stats = torch.empty(2, dtype=torch.float32, device=dev)
+        # sg_feed_t: sampler calls + label gather + label stats + packing in one launch
+        sadj, stypes, sn = self.store.to_device(dev)
+        smp = self.sampler
+        f = _lib.SgFeed()
+        if isinstance(smp, DeviceRandomSampler):
+            f.kind, f.state, f.sigma, f.n = 0, smp.state.data_ptr(), smp.sigma.data_ptr(), smp.n
+        else:
+            f.kind, f.state = 1, smp.state.data_ptr()
+            f.dens_order, f.bins = smp.dens_order.data_ptr(), smp.bins.data_ptr()
+            f.item_table, f.n_bins = smp.item_table.data_ptr(), int(smp.bins.numel())
+            f.bin_size = smp.bin_size
+        f.batch, f.compat = B, 1 if self.compat else 0
+        f.label_matrix, f.label_n = self.Y.data_ptr(), int(self.Y.shape[0])
+        f.store_adj, f.store_types, f.store_n = sadj.data_ptr(), stypes.data_ptr(), sn.data_ptr()
+        f.n_graphs, f.n_max = len(self.store), model.n_max
+        f.adj_dtype = _lib.dtype_code(model.record_dtype)
+        self._feed = f
 
     def next_batch(self):
-        """One step's batch (device only): the first B calls are the inputs, the
-        labels belong to the last B calls in 'compat' mode (quirk A3)."""
-        torch = self.torch
-        B = self.B
-        self.sampler.sample(self.count, self.pairs)
-        inp = self.pairs[:B]
-        lp = self.pairs[self.count - B:] if self.compat else inp
-        lab = self.Y[lp[:, 0].long(), lp[:, 1].long()]
-        pack_device_into(self.store, inp, lab, self.records, self.status,
-                         dtype=self.model.record_dtype)
-        return self.model.batch_from_records(self.records, B, lab)
+        """One step's batch (device only, one launch): the first B calls are the
+        inputs, the labels belong to the last B calls in 'compat' mode (quirk A3)."""
+        _lib.feed_step(self._feed, self.pairs, self.records, self.labels, self.y_stats,
+                       self.status)
+        return self.model.batch_from_records(self.records, self.B, self.labels,
+                                             y_stats=self.y_stats)
 
     def store_ids_to_graphs(self, ids):
         """Host bookkeeping: store ids -> ModelGraph objects."""

@@ -263,6 +263,33 @@ int32_t sg_sampler_density(int32_t *state, const int32_t *dens_order, const int3
                            int64_t count, int32_t *pairs_out, sg_stream_t stream);
 
 /*
+ * One step's get_feed_dict (model_mse.py:52-94) in one launch (library 1.5): the
+ * sampler calls (B + B² in compat mode, quirk A3; else B), the labels
+ * label_matrix[g1][g2] of the input pairs (compat: of the last B calls), the label
+ * statistics {ȳ, ½Σ(y-ȳ)²} (double accumulation, in order) and the B input records
+ * packed from the dense-slot store.  sg_feed_t is a host struct of device pointers.
+ * pairs_out holds count × 2 ids; status_out (may be NULL) gets SG_ERR_ARG for ids
+ * outside the store.
+ */
+typedef struct sg_feed {
+  int32_t kind;                 /* 0 RandomSampler (sigma, n), 1 DistributionSampler */
+  int32_t *state;               /* as sg_sampler_random / sg_sampler_density */
+  const int32_t *sigma;
+  int32_t n;
+  const int32_t *dens_order, *bins, *item_table;
+  int32_t n_bins, bin_size;
+  int32_t batch;                /* B */
+  int32_t compat;               /* 1: label stream of quirk A3 */
+  const float *label_matrix;    /* [label_n][label_n], indexed by store id */
+  int32_t label_n;
+  const float *store_adj;       /* dense-slot graph store (sg_pack_pairs) */
+  const int32_t *store_types, *store_n;
+  int32_t n_graphs, n_max, adj_dtype;
+} sg_feed_t;
+int32_t sg_feed_step(const sg_feed_t *feed, int32_t *pairs_out, void *records, float *labels_out,
+                     float *y_stats_out, int32_t *status_out, sg_stream_t stream);
+
+/*
  * Graph-store path for Web-sized graphs (library 1.5; BASELINE config C5).
  *
  * Pair records hold Â densely (n_max² per side), which stops scaling at a few
