@@ -252,9 +252,12 @@ __global__ void __launch_bounds__(256) web_wprep_h(const float *__restrict__ Wg,
 // are staged in LDS when they fit (one coalesced copy, then ~100-cycle reads in
 // the sparse loops instead of a dependent global-load chain per neighbour).
 // ---------------------------------------------------------------------------
-// waves per instance workgroup: 16 forward (2 tiles per wave), 8 backward (4 tiles
-// per wave: the backward needs more than the 128 VGPRs of a 16-wave block)
-__host__ __device__ constexpr int gcn_gw(bool bwd) { return bwd ? 8 : 16; }
+// waves per instance workgroup: 16 forward (2 tiles per wave), SG_WEB_BWD_WAVES backward
+// (the backward needs more than the 128 VGPRs of a 16-wave block)
+#ifndef SG_WEB_BWD_WAVES
+#define SG_WEB_BWD_WAVES 8
+#endif
+__host__ __device__ constexpr int gcn_gw(bool bwd) { return bwd ? SG_WEB_BWD_WAVES : 16; }
 
 struct GcnArgs {
   const int32_t *node_off, *types, *row_ptr, *col;
@@ -330,7 +333,7 @@ __device__ __forceinline__ void csr_row(const CT *__restrict__ col, const float 
 template <bool BWD, int NTB, bool LCSR>
 __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
   using ColT = typename std::conditional<LCSR, uint16_t, int>::type;
-  constexpr int GW_ = gcn_gw(BWD), NT = 64 * GW_, GCN_TPW = 32 / GW_;
+  constexpr int GW_ = gcn_gw(BWD), NT = 64 * GW_, GCN_TPW = (32 + GW_ - 1) / GW_;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   const int i = l & 15, g = l >> 4;
