@@ -41,6 +41,11 @@ constexpr int TS1 = 36;  // D1 tile row stride (floats)
 constexpr int TS2 = 20;  // gZ1 tile row stride
 constexpr int W1S = 20;  // W1 table row stride (16 + pad)
 constexpr int W1TS = 36; // W1ᵀ table row stride (32 + pad)
+// gD1 = gZ1·W1ᵀ on bf16 MFMA with both operands split in three parts (x = h + m + l,
+// the six leading products: ≈ f32 accuracy); W1's parts are built once per launch
+#ifndef SG_GD1_BF16
+#define SG_GD1_BF16 1
+#endif
 #ifndef SG_FAST_MAXW
 #define SG_FAST_MAXW 8
 #endif
@@ -84,7 +89,8 @@ struct FastLds {
   static constexpr int GE = X + 48;                   // AVG: ∂L/∂x1 | ∂L/∂x2 (16 each)
   static int wave_floats(int) { return X + 48 + (AVG ? 32 : 0); }
   static int shared_floats(int d_in) {
-    return (d_in + 1) * FH1 + 2 * DN * FK * WR + FK * VS + FH1 * W1S + FH2 * W1TS;
+    return (d_in + 1) * FH1 + 2 * DN * FK * WR + FK * VS + FH1 * W1S + FH2 * W1TS +
+           (SG_GD1_BF16 ? 2 * 3 * 64 * 4 : 0);
   }
 };
 
@@ -221,6 +227,9 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   float *sV = sWb + DN * FK * WR;               // [k][VS]
   float *sW1 = sV + FK * VS;                    // W1 · ik1 [32][16], row stride W1S (gD1)
   float *sW1T = sW1 + FH1 * W1S;                // W1ᵀ [16][32], row stride W1TS (Z1)
+  // [t][term][lane] bf16 B operands of gD1 (SG_GD1_BF16): lane (g, j) ↔ column 16t + j,
+  // k-slots 8g..8g+3 / 8g+4..8g+7 ↔ parts of W1[16t + j][4g..4g+3]·ik1
+  uint4 *sW1B = (uint4 *)(sW1T + FH2 * W1TS);
   float *W = smem + A.shared_floats + wv * A.wave_floats;
   float *sRec = W + L::REC;
   float *sT = W + L::TILE;
@@ -268,6 +277,18 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
     sW1[(i / FH2) * W1S + i % FH2] = w * A.ik1;
     sW1T[(i % FH2) * W1TS + i / FH2] = w;
   }
+#if SG_GD1_BF16
+  for (int i = tid; i < 2 * 3 * 64; i += blockDim.x) {
+    const int t = i / 192, term = (i / 64) % 3, ln = i & 63;
+    const int f = 16 * t + (ln & 15), k0 = 4 * (ln >> 4);
+    const float *wr = stg + A.oW1 + f * FH2 + k0;
+    uint32_t h01, m01, l01, h23, m23, l23;
+    split3(wr[0] * A.ik1, wr[1] * A.ik1, h01, m01, l01);
+    split3(wr[2] * A.ik1, wr[3] * A.ik1, h23, m23, l23);
+    sW1B[i] = term == 0 ? uint4{h01, h23, h01, h23}
+                        : (term == 1 ? uint4{m01, m23, h01, h23} : uint4{l01, l23, m01, m23});
+  }
+#endif
   // per-lane parameters, also from the staged copy
   const int j_ = tid & 15;
   const float b0v0 = stg[A.ob0 + j_], b0v1 = stg[A.ob0 + 16 + j_];
@@ -763,6 +784,32 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       }
       // gD1 · ik1 = gZ1 (W1 ik1)ᵀ per feature tile t (one chain per tile when packed)
       f4 gd[2][2];   // [side, or 0 = shared][t]
+#if SG_GD1_BF16
+      // A k-slots 8g..8g+7 = (h | m) or (h | l) of gZ1[i][4g..4g+3]; with the B parts
+      // (Wh | Wh), (Wm | Wh), (Wl | Wm): hh + mh + hm + lh + hl + mm in three MFMAs
+      uint4 ahm[2], ahl[2];
+#pragma unroll
+      for (int s = 0; s < (PACK ? 1 : 2); ++s) {
+        uint32_t h01, m01, l01, h23, m23, l23;
+        split3(gz1t[s][0], gz1t[s][1], h01, m01, l01);
+        split3(gz1t[s][2], gz1t[s][3], h23, m23, l23);
+        ahm[s] = uint4{h01, h23, m01, m23};
+        ahl[s] = uint4{h01, h23, l01, l23};
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const uint4 *wb = sW1B + t * 192 + l;
+        const uint4 b1 = wb[0], b2 = wb[64], b3 = wb[128];
+#pragma unroll
+        for (int s = 0; s < (PACK ? 1 : 2); ++s) {
+          f4 acc = {0.f, 0.f, 0.f, 0.f};
+          acc = mfbf(ahm[s], b1, acc);
+          acc = mfbf(ahl[s], b2, acc);
+          acc = mfbf(ahm[s], b3, acc);
+          gd[s][t] = acc;
+        }
+      }
+#else
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const f4 wt = *(const f4 *)(w1tp + 16 * t * W1S);
@@ -774,6 +821,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           gd[s][t] = acc;
         }
       }
+#endif
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int KS = s ? K1 : K0;
