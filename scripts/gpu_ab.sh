@@ -7,15 +7,16 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$ROOT"
-timeout -k 10 600 python -m pytest tests -q -x -m gpu > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 600 python -m pytest ${TESTS:-tests} -q -x -m gpu > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest_gpu rc=$rc"; tail -3 "$OUT/pytest_gpu.log"
 [ $rc -eq 0 ] || exit $rc
 # REPS rounds over the variants (alternating), 100 timed steps each
+# (BENCH_ARGS: extra bench.py flags, TESTS: pytest targets)
 REPS=${REPS:-2}
 for rep in $(seq 1 $REPS); do
   for lib in "$@"; do
     n=$(basename "$lib" .so)
-    SG_LIB=$ROOT/$lib timeout -k 10 300 python bench.py --cpu-sample -1 --steps 100 --warmup 10 \
+    SG_LIB=$ROOT/$lib timeout -k 10 300 python bench.py --cpu-sample -1 --steps 100 --warmup 10 ${BENCH_ARGS:-} \
       --json-out "$OUT/bench_${n}_$rep.json" > "$OUT/bench_${n}_$rep.log" 2>&1
     rc=$?
     [ $rc -eq 0 ] || { echo "bench $n rc=$rc"; exit $rc; }
