@@ -48,6 +48,11 @@ def parse():
                    help='record processing order: class-balanced (sg_pair_order) or batch order')
     p.add_argument('--chunk', type=int, default=4_000_000,
                    help='C4: pairs per packed chunk when a shard does not fit HBM')
+    p.add_argument('--source', choices=('auto', 'records'), default='auto',
+                   help='C4 streamed: the kernel gathers pairs from the graph store (auto) or '
+                        'packs records per chunk (records)')
+    p.add_argument('--store-chunk', type=int, default=25_000_000,
+                   help='C4 streamed from the store: pairs per launch')
     p.add_argument('--resident-gb', type=float, default=150.0,
                    help='C4: keep a shard\'s records resident up to this many GB')
     p.add_argument('--stack', choices=('default', 'average'), default='default',
@@ -138,8 +143,10 @@ def main():
         from graphembedding_amd.packer import record_words
         streamed = (b - a) * 4 * record_words(gs.n_max, args.records) > args.resident_gb * 1e9
     if streamed:
-        shard = AllPairsStream(gs, labels, srank, sworld, device=device, chunk=args.chunk,
-                               dtype=args.records, balance=balance)
+        store_src = args.source == 'auto' and model.kernel_path == 2 and args.records == 'f32'
+        shard = AllPairsStream(gs, labels, srank, sworld, device=device,
+                               chunk=args.store_chunk if store_src else args.chunk,
+                               dtype=args.records, balance=balance, source=args.source)
         batch = None
     if not web and not streamed:
         shard = AllPairsShard(gs, labels, srank, sworld, device=device, dtype=args.records)
@@ -244,8 +251,13 @@ def main():
             workload = ('AIDS10knef all-pairs (10,018 graphs, N <= 30, {:,} ordered '
                         'pairs), Padding/NTN 30' if c4 else
                         'AIDS700nef all-pairs (700 graphs, {:,} ordered pairs)').format(total_pairs)
-            inputs = ('packed in chunks of {} pairs inside the step'.format(shard.chunk)
-                      if streamed else 'records resident in HBM')
+            if streamed and shard.uses_store(model):
+                inputs = ('graph store resident in HBM; the kernel gathers each pair\'s graphs '
+                          '(no records), {} pairs per launch'.format(shard.chunk))
+            elif streamed:
+                inputs = 'packed in chunks of {} pairs inside the step'.format(shard.chunk)
+            else:
+                inputs = 'records resident in HBM'
             records = '{} Â, {} B/pair'.format(args.records, bytes_pair)
         out = {
             'metric': 'graph-pairs/sec (Siamese fwd+bwd), {} all-pairs'.format(name),

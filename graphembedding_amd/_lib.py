@@ -51,6 +51,14 @@ class SgCsrStore(ctypes.Structure):
                 ('max_nnz', ctypes.c_int32)]
 
 
+class SgPairSource(ctypes.Structure):
+    """sg_pair_source_t: host struct of device pointers (store-sourced pairs, library 1.6)."""
+    _fields_ = [('adj', ctypes.c_void_p), ('types', ctypes.c_void_p), ('n', ctypes.c_void_p),
+                ('n_graphs', ctypes.c_int32), ('n_max', ctypes.c_int32),
+                ('pair_idx', ctypes.c_void_p), ('grid_base', ctypes.c_int64),
+                ('labels', ctypes.c_void_p), ('status', ctypes.c_void_p)]
+
+
 class SgFeed(ctypes.Structure):
     """sg_feed_t: host struct of device pointers (one step's get_feed_dict)."""
     _fields_ = [('kind', ctypes.c_int32), ('state', ctypes.c_void_p), ('sigma', ctypes.c_void_p),
@@ -143,6 +151,14 @@ def lib():
     L.sg_web_fwd_bwd.argtypes = [pm, pc, vp, vp, c_i64, c_i64, c_i64, vp, c_u64, vp, c_i32, vp,
                                  vp, vp, vp, c_i64, vp]
     L.sg_web_fwd_bwd.restype = c_i32
+    ps = ctypes.POINTER(SgPairSource)
+    L.sg_pair_order_src.argtypes = [pm, ps, c_i64, vp, vp, vp]
+    L.sg_pair_order_src.restype = c_i32
+    L.sg_forward_src.argtypes = [pm, ps, vp, c_i64, c_i64, vp, c_u64, vp, vp, vp]
+    L.sg_forward_src.restype = c_i32
+    L.sg_fwd_bwd_src.argtypes = [pm, ps, vp, c_i64, c_i64, c_i64, vp, c_u64, vp, c_i32, vp, vp,
+                                 vp, vp, vp]
+    L.sg_fwd_bwd_src.restype = c_i32
     _lib = L
     return L
 
@@ -157,7 +173,7 @@ EXPORTED_SYMBOLS = ('sg_version', 'sg_record_bytes', 'sg_record_bytes_ex', 'sg_m
                     'sg_pair_order_workspace_bytes', 'sg_sampler_random', 'sg_sampler_density',
                     'sg_adam_workspace_bytes', 'sg_adam_tf_ex', 'sg_web_workspace_bytes',
                     'sg_web_forward', 'sg_web_fwd_bwd', 'sg_fwd_bwd_dseed', 'sg_seed_advance',
-                    'sg_feed_step')
+                    'sg_feed_step', 'sg_pair_order_src', 'sg_forward_src', 'sg_fwd_bwd_src')
 
 # sg_dtype: storage type of Â in the pair records
 DTYPES = {'f32': 0, 'bf16': 1}
@@ -320,6 +336,38 @@ def fwd_bwd_dseed(m: SgModel, records, n_pairs, pair_offset, batch_total, params
                                  _ptr(y_stats), int(add_label_term), _ptr(s_out), _ptr(grad_out),
                                  _ptr(loss_out), _ptr(workspace), _stream(stream)),
           'sg_fwd_bwd_dseed')
+
+
+def pair_source(store_dev, n_max, pair_idx=None, grid_base=0, labels=None, status=None):
+    """sg_pair_source_t over a device dense store (adj, types, n) = GraphStore.to_device();
+    pair_idx int32 [n, 2] or None for the all-pairs grid from grid_base.  The struct
+    holds raw pointers: keep the tensors alive while it is in use."""
+    adj, types, n = store_dev
+    return SgPairSource(_ptr(adj), _ptr(types), _ptr(n), int(n.numel()), int(n_max),
+                        _ptr(pair_idx), int(grid_base), _ptr(labels), _ptr(status))
+
+
+def pair_order_src(m: SgModel, src: SgPairSource, n_pairs, order_out, workspace, stream=None):
+    check(lib().sg_pair_order_src(ctypes.byref(m), ctypes.byref(src), int(n_pairs),
+                                  _ptr(order_out), _ptr(workspace), _stream(stream)),
+          'sg_pair_order_src')
+
+
+def forward_src(m: SgModel, src: SgPairSource, n_pairs, pair_offset, params, seed, s_out,
+                workspace=None, stream=None, order=None):
+    check(lib().sg_forward_src(ctypes.byref(m), ctypes.byref(src), _ptr(order), int(n_pairs),
+                               int(pair_offset), _ptr(params), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                               _ptr(s_out), _ptr(workspace), _stream(stream)), 'sg_forward_src')
+
+
+def fwd_bwd_src(m: SgModel, src: SgPairSource, n_pairs, pair_offset, batch_total, params, seed,
+                y_stats, add_label_term, s_out, grad_out, loss_out, workspace, stream=None,
+                order=None):
+    check(lib().sg_fwd_bwd_src(ctypes.byref(m), ctypes.byref(src), _ptr(order), int(n_pairs),
+                               int(pair_offset), int(batch_total), _ptr(params),
+                               int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(y_stats), int(add_label_term),
+                               _ptr(s_out), _ptr(grad_out), _ptr(loss_out), _ptr(workspace),
+                               _stream(stream)), 'sg_fwd_bwd_src')
 
 
 def seed_advance(seed_dev, delta=1, stream=None):

@@ -132,11 +132,16 @@ class AllPairsStream(object):
     are those of the unchunked step.  The chunk gradients and losses are summed in
     chunk order (deterministic), leaving model.grad / model.loss_buf as one fwd_bwd
     over the whole shard would (up to fp32 summation order).
+
+    source='auto' skips the records when the model runs the fused capacity-32 kernel
+    with f32 Â (config C4): the kernel then gathers every pair's graphs from the store
+    (sg_fwd_bwd_src, library 1.6) and the pack pass with its 8.5 KB-per-pair write and
+    read-back disappears.  source='records' always packs.
     """
 
     def __init__(self, gs: GraphSet, labels: np.ndarray, rank: int = 0, world: int = 1,
                  device='cuda', chunk: int = 4_000_000, dtype: str = 'f32',
-                 n_pairs: Optional[int] = None, balance: bool = True):
+                 n_pairs: Optional[int] = None, balance: bool = True, source: str = 'auto'):
         import torch
         self.torch = torch
         G = len(gs.graphs)
@@ -157,19 +162,33 @@ class AllPairsStream(object):
         self.y_stats = torch.tensor([ybar, 0.5 * ((y - ybar) ** 2).sum()], dtype=torch.float32,
                                     device=device)
         self.record_bytes = 4 * record_words(gs.n_max, dtype)
-        self.records = torch.empty(self.chunk * record_words(gs.n_max, dtype), dtype=torch.int32,
-                                   device=device)
+        if source not in ('auto', 'records'):
+            raise RuntimeError('Unknown pair source {}'.format(source))
+        self.source = source
+        self.records = None   # allocated on the first packed chunk
         self.status = torch.zeros(1, dtype=torch.int32, device=device)
 
     def chunks(self):
         for c0 in range(self.start, self.end, self.chunk):
             yield c0, min(self.chunk, self.end - c0)
 
+    def uses_store(self, model) -> bool:
+        return (self.source == 'auto' and model.kernel_path == 2 and self.dtype == 'f32' and
+                model.record_dtype == 'f32' and self.store.n_max == model.n_max)
+
     def _pack(self, model, c0: int, n: int):
         torch = self.torch
+        lab = self.labels[c0 - self.start:c0 - self.start + n]
+        if self.uses_store(model):
+            b = model.batch_from_store(self.store, n, lab, grid_base=c0, pair_offset=c0,
+                                       batch_total=self.total, y_stats=self.y_stats,
+                                       status=self.status)
+            return model.balance(b) if self.balance else b
+        if self.records is None:
+            self.records = torch.empty(self.chunk * record_words(self.store.n_max, self.dtype),
+                                       dtype=torch.int32, device=self.device)
         p = torch.arange(c0, c0 + n, dtype=torch.int64, device=self.device)
         pi = torch.stack([p // self.G, p % self.G], dim=1).to(torch.int32).contiguous()
-        lab = self.labels[c0 - self.start:c0 - self.start + n]
         pack_device_into(self.store, pi, lab, self.records, self.status, dtype=self.dtype)
         b = model.batch_from_records(self.records, n, lab, pair_offset=c0,
                                      batch_total=self.total, y_stats=self.y_stats)

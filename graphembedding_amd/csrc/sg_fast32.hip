@@ -70,7 +70,31 @@ struct F32Args {
   int d_in, n_params, D;
   int shared_floats, wave_floats;
   int oW0, ob0, oW1, ob1, oWd, obd, oW, oV, oU, obn;
+  // pair source (sg_pair_source_t): src_store = 1 gathers each pair from the dense
+  // graph store instead of reading a packed record
+  int src_store, G;
+  const uint4 *sadj, *stypes;   // [G][NC·NC/4], [G][NC/4] 16-B words
+  const int32_t *sn, *spairs;   // [G], [n_pairs][2] or NULL (all-pairs grid)
+  int64_t grid_base;
+  const float *slabels;
+  int32_t *status;
 };
+
+// Graph ids of local pair p of a store-sourced launch (all lanes, wave-uniform);
+// false for ids outside [0, G) (the pair then reads as a zero record)
+__device__ __forceinline__ bool f32_pair_ids(const F32Args &A, int p, int &g0, int &g1) {
+  if (A.spairs) {
+    g0 = A.spairs[2 * (int64_t)p];
+    g1 = A.spairs[2 * (int64_t)p + 1];
+  } else {
+    const int64_t q = A.grid_base + p;
+    g0 = (int)(q / A.G);
+    g1 = (int)(q - (int64_t)g0 * A.G);
+  }
+  const bool ok = (unsigned)g0 < (unsigned)A.G && (unsigned)g1 < (unsigned)A.G;
+  if (!ok) g0 = g1 = 0;
+  return ok;
+}
 
 // per-wave LDS (floats): record image (Â rows at stride RS, then types, n, label,
 // tag) | D1 transpose tile (one side) | x1 | x2 | pad
@@ -222,13 +246,38 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
     }
     // ---- stage the record (f32 LDS image; bf16 Â widened) ----
     {
-      const uint4 *src = (const uint4 *)(A.recs + (size_t)(uint32_t)p * (size_t)rw4h * 16u);
       constexpr int NREC = (RW4 + 63) / 64;
       uint4 v[NREC];
+      if (A.src_store) {
+        // the record's 16-B words from the store: Â of g0 | Â of g1 | types of g0 |
+        // types of g1 | (n0, n1, label, tag) — the layout sg_pack_pairs writes
+        int g0, g1;
+        const bool ok = f32_pair_ids(A, p, g0, g1);
+        if (!ok && l == 0 && A.status) atomicExch(A.status, (int32_t)SG_ERR_ARG);
+        const uint4 *a0 = A.sadj + (size_t)g0 * ADJ4, *a1 = A.sadj + (size_t)g1 * ADJ4;
+        const uint4 *t0 = A.stypes + (size_t)g0 * (NC / 4), *t1 = A.stypes + (size_t)g1 * (NC / 4);
 #pragma unroll
-      for (int c = 0; c < NREC; ++c) {
-        const int w4 = l + 64 * c;
-        v[c] = w4 < rw4h ? src[w4] : uint4{0u, 0u, 0u, 0u};
+        for (int c = 0; c < NREC; ++c) {
+          const int w4 = l + 64 * c;
+          uint4 x = uint4{0u, 0u, 0u, 0u};
+          if (ok) {
+            if (w4 < ADJ4) x = a0[w4];
+            else if (w4 < 2 * ADJ4) x = a1[w4 - ADJ4];
+            else if (w4 < 2 * ADJ4 + NC / 4) x = t0[w4 - 2 * ADJ4];
+            else if (w4 < 2 * ADJ4 + NC / 2) x = t1[w4 - 2 * ADJ4 - NC / 4];
+            else if (w4 == 2 * ADJ4 + NC / 2)
+              x = uint4{(uint32_t)A.sn[g0], (uint32_t)A.sn[g1],
+                        __float_as_uint(A.slabels ? A.slabels[p] : 0.f), (uint32_t)p};
+          }
+          v[c] = x;
+        }
+      } else {
+        const uint4 *src = (const uint4 *)(A.recs + (size_t)(uint32_t)p * (size_t)rw4h * 16u);
+#pragma unroll
+        for (int c = 0; c < NREC; ++c) {
+          const int w4 = l + 64 * c;
+          v[c] = w4 < rw4h ? src[w4] : uint4{0u, 0u, 0u, 0u};
+        }
       }
       sg_wsync();   // the previous pair's LDS reads are done
       // HBM word w of the Â block (row r = w / NC, column w % NC) -> LDS r·RS + w % NC
@@ -834,11 +883,24 @@ int sg_ntn_wgrad_run(const float *ntn, int64_t n_pairs, int D, int oW, int oV, i
 int sg_fast32_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
                   const int32_t *order, int64_t n_pairs, int64_t pair_offset,
                   int64_t batch_total, const float *params, uint64_t seed, const float *y_stats,
-                  float *s_out, float *slab, float *ntn, int *blocks_out, hipStream_t stream) {
+                  float *s_out, float *slab, float *ntn, int *blocks_out, hipStream_t stream,
+                  const sg_pair_source_t *src) {
   const F32Cfg c = f32_cfg(P, n_pairs, bwd);
   if (n_pairs > 0x7FFFFFFF - (int64_t)c.blocks * c.waves * 2) return SG_ERR_ARG;
   F32Args A;
   A.recs = (const uint8_t *)recs;
+  A.src_store = src ? 1 : 0;
+  A.G = src ? src->n_graphs : 0;
+  A.sadj = src ? (const uint4 *)src->adj : nullptr;
+  A.stypes = src ? (const uint4 *)src->types : nullptr;
+  A.sn = src ? src->n : nullptr;
+  A.spairs = src ? src->pair_idx : nullptr;
+  A.grid_base = src ? src->grid_base : 0;
+  A.slabels = src ? src->labels : nullptr;
+  A.status = src ? src->status : nullptr;
+  if (src && (P.adj_dtype != SG_DTYPE_F32 || src->n_max != NC || src->n_graphs <= 0 ||
+              !src->adj || !src->types || !src->n))
+    return SG_ERR_ARG;
   A.order = order;
   A.n_pairs = n_pairs;
   A.pair_offset = pair_offset;

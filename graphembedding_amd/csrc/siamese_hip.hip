@@ -53,7 +53,8 @@ int64_t sg_fast32_ntn_floats(int64_t n_pairs);
 int sg_fast32_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
                   const int32_t *order, int64_t n_pairs, int64_t pair_offset,
                   int64_t batch_total, const float *params, uint64_t seed, const float *y_stats,
-                  float *s_out, float *slab, float *ntn, int *blocks_out, hipStream_t stream);
+                  float *s_out, float *slab, float *ntn, int *blocks_out, hipStream_t stream,
+                  const sg_pair_source_t *src = nullptr);
 
 namespace {
 
@@ -205,10 +206,40 @@ __global__ void __launch_bounds__(256) sg_pack_kernel(const float *__restrict__ 
 constexpr int kOrderChunk = 8192;   // records per block
 constexpr int kOrderKeys = 129;     // 2·n_max + 1 keys at n_max ≤ 64
 
-__device__ __forceinline__ int sg_order_key(const uint8_t *__restrict__ recs, int64_t p,
-                                            int rec_words, int n_off, int nmax, int fast) {
-  const int32_t *r = (const int32_t *)(recs + (size_t)p * (size_t)rec_words * 4u) + n_off;
-  int n0 = r[0], n1 = r[1];
+// Node counts of pair p: from its packed record, or from the store (pair source)
+struct OrderRecs {
+  const uint8_t *recs;
+  int rec_words, n_off;
+  __device__ void n01(int64_t p, int &n0, int &n1) const {
+    const int32_t *r = (const int32_t *)(recs + (size_t)p * (size_t)rec_words * 4u) + n_off;
+    n0 = r[0];
+    n1 = r[1];
+  }
+};
+struct OrderStore {
+  const int32_t *sn, *pairs;
+  int64_t grid_base;
+  int G;
+  __device__ void n01(int64_t p, int &n0, int &n1) const {
+    int g0, g1;
+    if (pairs) {
+      g0 = pairs[2 * p];
+      g1 = pairs[2 * p + 1];
+    } else {
+      const int64_t q = grid_base + p;
+      g0 = (int)(q / G);
+      g1 = (int)(q - (int64_t)g0 * G);
+    }
+    const bool ok = (unsigned)g0 < (unsigned)G && (unsigned)g1 < (unsigned)G;
+    n0 = ok ? sn[g0] : 0;   // invalid ids read as a zero record
+    n1 = ok ? sn[g1] : 0;
+  }
+};
+
+template <class S>
+__device__ __forceinline__ int sg_order_key(const S &src, int64_t p, int nmax, int fast) {
+  int n0, n1;
+  src.n01(p, n0, n1);
   n0 = n0 < 0 ? 0 : (n0 > nmax ? nmax : n0);
   n1 = n1 < 0 ? 0 : (n1 > nmax ? nmax : n1);
   // fast: 1 = sg_fast (third k-step per side), 2 = sg_fast32 (k-blocks of 4 nodes)
@@ -216,16 +247,15 @@ __device__ __forceinline__ int sg_order_key(const uint8_t *__restrict__ recs, in
   return fast ? (n0 > 8) + (n1 > 8) : n0 + n1;
 }
 
-__global__ void __launch_bounds__(256) sg_order_count(const uint8_t *__restrict__ recs, int64_t n,
-                                                      int rec_words, int n_off, int nmax,
-                                                      int fast, int K, int nb,
-                                                      int32_t *__restrict__ cnt) {
+template <class S>
+__global__ void __launch_bounds__(256) sg_order_count(S src, int64_t n, int nmax, int fast, int K,
+                                                      int nb, int32_t *__restrict__ cnt) {
   __shared__ int h[kOrderKeys];
   for (int k = threadIdx.x; k < K; k += blockDim.x) h[k] = 0;
   __syncthreads();
   const int64_t b0 = (int64_t)blockIdx.x * kOrderChunk;
   for (int i = threadIdx.x; i < kOrderChunk && b0 + i < n; i += blockDim.x)
-    atomicAdd(&h[sg_order_key(recs, b0 + i, rec_words, n_off, nmax, fast)], 1);
+    atomicAdd(&h[sg_order_key(src, b0 + i, nmax, fast)], 1);
   __syncthreads();
   for (int k = threadIdx.x; k < K; k += blockDim.x) cnt[(size_t)k * nb + blockIdx.x] = h[k];
 }
@@ -255,9 +285,9 @@ __global__ void __launch_bounds__(1024) sg_order_scan(int32_t *__restrict__ a, i
   }
 }
 
-__global__ void __launch_bounds__(256) sg_order_scatter(const uint8_t *__restrict__ recs, int64_t n,
-                                                        int rec_words, int n_off, int nmax,
-                                                        int fast, int K, int nb,
+template <class S>
+__global__ void __launch_bounds__(256) sg_order_scatter(S src, int64_t n, int nmax, int fast,
+                                                        int K, int nb,
                                                         const int32_t *__restrict__ base,
                                                         int32_t *__restrict__ order) {
   __shared__ int run[kOrderKeys];
@@ -271,7 +301,7 @@ __global__ void __launch_bounds__(256) sg_order_scatter(const uint8_t *__restric
     __syncthreads();
     const int64_t p = t0 + t;
     const bool valid = p < b1;
-    const int key = valid ? sg_order_key(recs, p, rec_words, n_off, nmax, fast) : -1;
+    const int key = valid ? sg_order_key(src, p, nmax, fast) : -1;
     // rank among the earlier lanes of this wave with the same key
     int rank = 0;
     uint64_t active = __ballot(valid);
@@ -458,7 +488,7 @@ int64_t ntn_offset_floats(const PathChoice &c, int64_t n_pairs) {
 // ===========================================================================
 extern "C" {
 
-int32_t sg_version(void) { return 10500; }   /* 1.5.0: graph-store path (config C5) */
+int32_t sg_version(void) { return 10600; }   /* 1.6.0: store-sourced pairs (sg_*_src) */
 
 int64_t sg_record_bytes(int32_t n_max) { return sg_record_bytes_ex(n_max, SG_DTYPE_F32); }
 
@@ -555,6 +585,20 @@ int64_t sg_pair_order_workspace_bytes(const sg_model_t *model, int64_t n_pairs) 
   return nb * kOrderKeys * 4 + 256;
 }
 
+extern "C++" template <class S>
+static int32_t launch_order(S src, int nmax, int fast, int64_t n_pairs, int32_t *order_out,
+                            void *workspace, hipStream_t st) {
+  const int K = fast == 1 ? 3 : (fast == 2 ? 2 * ((nmax + 3) / 4) + 1 : 2 * nmax + 1);
+  const int nb = (int)((n_pairs + kOrderChunk - 1) / kOrderChunk);
+  int32_t *cnt = (int32_t *)workspace;
+  hipLaunchKernelGGL(sg_order_count<S>, dim3(nb), dim3(256), 0, st, src, n_pairs, nmax, fast, K,
+                     nb, cnt);
+  hipLaunchKernelGGL(sg_order_scan, dim3(1), dim3(1024), 0, st, cnt, (int64_t)K * nb);
+  hipLaunchKernelGGL(sg_order_scatter<S>, dim3(nb), dim3(256), 0, st, src, n_pairs, nmax, fast, K,
+                     nb, (const int32_t *)cnt, order_out);
+  return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
+}
+
 int32_t sg_pair_order(const sg_model_t *model, const void *records, int64_t n_pairs,
                       int32_t *order_out, void *workspace, sg_stream_t stream) {
   if (n_pairs < 0 || n_pairs > 0x7FFFFFFF) return SG_ERR_ARG;
@@ -564,18 +608,31 @@ int32_t sg_pair_order(const sg_model_t *model, const void *records, int64_t n_pa
   if (c.status != SG_OK) return c.status;
   const int nmax = c.plan.n_max;
   const SgRecLayout rl = sg_rec_layout(nmax, c.plan.adj_dtype);
-  const int n_off = rl.adj_words + 2 * nmax;
-  const int fast = c.path;
-  const int K = fast == 1 ? 3 : (fast == 2 ? 2 * ((nmax + 3) / 4) + 1 : 2 * nmax + 1);
-  const int nb = (int)((n_pairs + kOrderChunk - 1) / kOrderChunk);
-  hipStream_t st = (hipStream_t)stream;
-  int32_t *cnt = (int32_t *)workspace;
-  hipLaunchKernelGGL(sg_order_count, dim3(nb), dim3(256), 0, st, (const uint8_t *)records, n_pairs,
-                     rl.words, n_off, nmax, fast, K, nb, cnt);
-  hipLaunchKernelGGL(sg_order_scan, dim3(1), dim3(1024), 0, st, cnt, (int64_t)K * nb);
-  hipLaunchKernelGGL(sg_order_scatter, dim3(nb), dim3(256), 0, st, (const uint8_t *)records,
-                     n_pairs, rl.words, n_off, nmax, fast, K, nb, (const int32_t *)cnt, order_out);
-  return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
+  OrderRecs src{(const uint8_t *)records, rl.words, rl.adj_words + 2 * nmax};
+  return launch_order(src, nmax, c.path, n_pairs, order_out, workspace, (hipStream_t)stream);
+}
+
+// a store-sourced call's checks: fused capacity-32 path, f32 Â, store shape = n_max
+static int32_t src_check(const PathChoice &c, const sg_pair_source_t *src) {
+  if (!src || !src->adj || !src->types || !src->n || src->n_graphs <= 0) return SG_ERR_ARG;
+  if (c.path != 2 || c.plan.adj_dtype != SG_DTYPE_F32) return SG_ERR_UNSUPPORTED;
+  if (src->n_max != c.plan.n_max || src->grid_base < 0) return SG_ERR_ARG;
+  return SG_OK;
+}
+
+int32_t sg_pair_order_src(const sg_model_t *model, const sg_pair_source_t *src,
+                          int64_t n_pairs, int32_t *order_out, void *workspace,
+                          sg_stream_t stream) {
+  if (n_pairs < 0 || n_pairs > 0x7FFFFFFF) return SG_ERR_ARG;
+  PathChoice c = choose_path(model, true);
+  if (c.status != SG_OK) return c.status;
+  const int32_t rc = src_check(c, src);
+  if (rc != SG_OK) return rc;
+  if (n_pairs == 0) return SG_OK;
+  if (!order_out || !workspace) return SG_ERR_ARG;
+  OrderStore os{src->n, src->pair_idx, src->grid_base, src->n_graphs};
+  return launch_order(os, c.plan.n_max, c.path, n_pairs, order_out, workspace,
+                      (hipStream_t)stream);
 }
 
 int32_t sg_forward(const sg_model_t *model, const void *records, int64_t n_pairs,
@@ -619,12 +676,16 @@ static int32_t fwd_bwd_impl(const sg_model_t *model, const void *records, const 
                             const float *params, uint64_t seed, const uint64_t *seed_dev,
                             const float *y_stats, int32_t add_label_term, float *s_out,
                             float *grad_out, float *loss_out, void *workspace,
-                            sg_stream_t stream) {
+                            sg_stream_t stream, const sg_pair_source_t *src = nullptr) {
   if (n_pairs < 0 || pair_offset < 0) return SG_ERR_ARG;
   if (order && n_pairs > 0x7FFFFFFF) return SG_ERR_ARG;
   if (!params || !grad_out || !workspace) return SG_ERR_ARG;
   PathChoice c = choose_path(model, true);
   if (c.status != SG_OK) return c.status;
+  if (src) {
+    const int32_t rc = src_check(c, src);
+    if (rc != SG_OK) return rc;
+  }
   if (seed_dev && c.path != 1) return SG_ERR_UNSUPPORTED;   // device seed: fused path only
   if (model->loss_mode == SG_LOSS_BROADCAST && !y_stats) return SG_ERR_ARG;
   if (model->loss_mode == SG_LOSS_ALIGNED && batch_total <= 0) return SG_ERR_ARG;
@@ -637,7 +698,7 @@ static int32_t fwd_bwd_impl(const sg_model_t *model, const void *records, const 
     if (loss_out && hipMemsetAsync(loss_out, 0, 4u, st) != hipSuccess) return SG_ERR_HIP;
     return SG_OK;
   }
-  if (!records) return SG_ERR_ARG;
+  if (!records && !src) return SG_ERR_ARG;
   int nblk = 0;
   int rc;
   if (c.path == 1)
@@ -647,7 +708,7 @@ static int32_t fwd_bwd_impl(const sg_model_t *model, const void *records, const 
   else if (c.path == 2)
     rc = sg_fast32_run(model, c.plan, true, records, order, n_pairs, pair_offset, batch_total,
                        params, seed, y_stats, s_out, slab, slab + ntn_offset_floats(c, n_pairs),
-                       &nblk, st);
+                       &nblk, st, src);
   else
     rc = sg_generic_run(c.plan, true, records, order, n_pairs, pair_offset, batch_total, params,
                         seed, y_stats, s_out, slab, &nblk, st);
@@ -665,6 +726,34 @@ int32_t sg_fwd_bwd_ex(const sg_model_t *model, const void *records, const int32_
   return fwd_bwd_impl(model, records, order, n_pairs, pair_offset, batch_total, params, seed,
                       nullptr, y_stats, add_label_term, s_out, grad_out, loss_out, workspace,
                       stream);
+}
+
+int32_t sg_fwd_bwd_src(const sg_model_t *model, const sg_pair_source_t *src,
+                       const int32_t *order, int64_t n_pairs, int64_t pair_offset,
+                       int64_t batch_total, const float *params, uint64_t seed,
+                       const float *y_stats, int32_t add_label_term, float *s_out,
+                       float *grad_out, float *loss_out, void *workspace, sg_stream_t stream) {
+  if (!src) return SG_ERR_ARG;
+  return fwd_bwd_impl(model, nullptr, order, n_pairs, pair_offset, batch_total, params, seed,
+                      nullptr, y_stats, add_label_term, s_out, grad_out, loss_out, workspace,
+                      stream, src);
+}
+
+int32_t sg_forward_src(const sg_model_t *model, const sg_pair_source_t *src,
+                       const int32_t *order, int64_t n_pairs, int64_t pair_offset,
+                       const float *params, uint64_t seed, float *s_out, void *workspace,
+                       sg_stream_t stream) {
+  (void)workspace;
+  if (n_pairs < 0 || pair_offset < 0) return SG_ERR_ARG;
+  if (order && n_pairs > 0x7FFFFFFF) return SG_ERR_ARG;
+  PathChoice c = choose_path(model, false);
+  if (c.status != SG_OK) return c.status;
+  const int32_t rc = src_check(c, src);
+  if (rc != SG_OK) return rc;
+  if (n_pairs == 0) return SG_OK;
+  if (!params || !s_out) return SG_ERR_ARG;
+  return sg_fast32_run(model, c.plan, false, nullptr, order, n_pairs, pair_offset, n_pairs, params,
+                       seed, nullptr, s_out, nullptr, nullptr, nullptr, (hipStream_t)stream, src);
 }
 
 int32_t sg_fwd_bwd_dseed(const sg_model_t *model, const void *records, const int32_t *order,

@@ -77,6 +77,10 @@ class Batch:
     csr: object = None              # web.CsrStore
     pairs: object = None            # torch.int32 [n, 2] store graph ids
     chunk: int = 0                  # pairs per internal chunk (workspace size)
+    # store-sourced pairs (library 1.6, kernel path 2): the fused kernel gathers each pair
+    # from a dense GraphStore instead of a packed record (records is None)
+    src: object = None              # _lib.SgPairSource
+    src_keep: tuple = ()            # the device tensors src points into (kept alive)
 
 
 class SiameseGCNTNMSE(object):
@@ -157,6 +161,10 @@ class SiameseGCNTNMSE(object):
             _lib.web_forward(self.sg, batch.csr.to_device(self.device), batch.pairs, batch.n_pairs,
                              batch.pair_offset, self.params, self._seed(seed), s,
                              self.web_workspace(batch.chunk), batch.chunk)
+            return s
+        if batch.src is not None:
+            _lib.forward_src(self.sg, batch.src, batch.n_pairs, batch.pair_offset, self.params,
+                             self._seed(seed), s, order=batch.order)
             return s
         _lib.forward(self.sg, batch.records, batch.n_pairs, batch.pair_offset, self.params,
                      self._seed(seed), s, order=batch.order)
@@ -270,6 +278,28 @@ class SiameseGCNTNMSE(object):
                      batch_total=int(batch_total if batch_total is not None else n_pairs),
                      gid_pairs=gid_pairs)
 
+    def batch_from_store(self, store, n_pairs, labels, pair_idx=None, grid_base=0,
+                         pair_offset=0, batch_total=None, y_stats=None, status=None) -> Batch:
+        """A batch whose pairs the fused kernel gathers from the dense store itself
+        (sg_*_src, library 1.6; kernel path 2 with f32 Â): store = packer.GraphStore,
+        pair_idx int32 [n, 2] device tensor or None for the all-pairs grid (pair i =
+        divmod(grid_base + i, G)), labels float32 [n] device tensor.  Same results as
+        packing the pairs into records (sg_pack_pairs) and stepping those."""
+        if self.kernel_path != 2 or self.record_dtype != 'f32':
+            raise _lib.SiameseHipError('store-sourced batches need the fused capacity-32 '
+                                       'path with f32 records (kernel path {})'.format(
+                                           self.kernel_path))
+        if store.n_max != self.n_max:
+            raise _lib.SiameseHipError('store n_max {} != model n_max {}'.format(store.n_max,
+                                                                                 self.n_max))
+        dev = store.to_device(self.device)
+        b = self.batch_from_records(None, n_pairs, labels, pair_offset=pair_offset,
+                                    batch_total=batch_total, y_stats=y_stats)
+        b.src = _lib.pair_source(dev, store.n_max, pair_idx=pair_idx, grid_base=grid_base,
+                                 labels=b.labels, status=status)
+        b.src_keep = (dev, pair_idx, b.labels, status)
+        return b
+
     # ---- steps ----------------------------------------------------------------
     def _seed(self, seed):
         return (self.seed * 1000003 + self.step_count) if seed is None else int(seed)
@@ -292,6 +322,12 @@ class SiameseGCNTNMSE(object):
                              self.grad, self.loss_buf, self.web_workspace(batch.chunk),
                              batch.chunk)
             return
+        if batch.src is not None:
+            _lib.fwd_bwd_src(self.sg, batch.src, batch.n_pairs, batch.pair_offset,
+                             batch.batch_total, self.params, self._seed(seed), batch.y_stats,
+                             1 if add_label_term else 0, s_out, self.grad, self.loss_buf,
+                             self.workspace(batch.n_pairs), order=batch.order)
+            return
         _lib.fwd_bwd(self.sg, batch.records, batch.n_pairs, batch.pair_offset,
                      batch.batch_total, self.params, self._seed(seed), batch.y_stats,
                      1 if add_label_term else 0, s_out, self.grad, self.loss_buf,
@@ -309,7 +345,10 @@ class SiameseGCNTNMSE(object):
         ws = torch.empty(_lib.pair_order_workspace_bytes(self.sg, batch.n_pairs) // 4 + 1,
                          dtype=torch.int32, device=self.device)
         order = torch.empty(batch.n_pairs, dtype=torch.int32, device=self.device)
-        _lib.pair_order(self.sg, batch.records, batch.n_pairs, order, ws)
+        if batch.src is not None:
+            _lib.pair_order_src(self.sg, batch.src, batch.n_pairs, order, ws)
+        else:
+            _lib.pair_order(self.sg, batch.records, batch.n_pairs, order, ws)
         batch.order = order
         return batch
 

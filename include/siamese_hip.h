@@ -366,6 +366,52 @@ int32_t sg_adam_tf_ex(float *params, float *m, float *v, const float *grad, int6
                       float beta1, float beta2, float eps, float weight_decay, float *beta_powers,
                       float *reg_loss_out, void *workspace, sg_stream_t stream);
 
+/*
+ * Pairs straight from the dense graph store (library 1.6).  sg_pack_pairs writes a
+ * record per pair that the fused kernel then reads back: for a stream that does not
+ * fit HBM at once (config C4, AIDS10knef all-pairs: 100.4 M pairs, 850 GB of
+ * records) that round trip is a quarter of the step.  These calls take the
+ * sg_pack_pairs inputs instead and the kernel gathers each pair's two graphs from
+ * the store itself (41 MB at C4: cache-resident).  Same pair ids, labels, dropout
+ * keys, order and results as packing + sg_fwd_bwd_ex bit for bit.
+ *
+ * sg_pair_source_t is a HOST struct holding DEVICE pointers:
+ *   adj [n_graphs][n_max][n_max] f32, types [n_graphs][n_max] i32, n [n_graphs] i32
+ *       (the sg_pack_pairs store);
+ *   pair_idx  [n_pairs][2] i32 graph ids, or NULL: the all-pairs grid, pair i =
+ *             (q / n_graphs, q % n_graphs) with q = grid_base + i (row-major);
+ *   labels    [n_pairs] f32 or NULL (label := 0);
+ *   status    device int or NULL: invalid graph ids set SG_ERR_ARG and read as a
+ *             zero record, as in sg_pack_pairs.
+ * Fused capacity-32 path (sg_model_validate path 2) with f32 Â only; other models
+ * give SG_ERR_UNSUPPORTED.  Workspace sizes are sg_workspace_bytes /
+ * sg_pair_order_workspace_bytes.
+ */
+typedef struct sg_pair_source {
+  const float *adj;
+  const int32_t *types;
+  const int32_t *n;
+  int32_t n_graphs;
+  int32_t n_max;
+  const int32_t *pair_idx;
+  int64_t grid_base;
+  const float *labels;
+  int32_t *status;
+} sg_pair_source_t;
+
+int32_t sg_pair_order_src(const sg_model_t *model, const sg_pair_source_t *src,
+                          int64_t n_pairs, int32_t *order_out, void *workspace,
+                          sg_stream_t stream);
+int32_t sg_forward_src(const sg_model_t *model, const sg_pair_source_t *src,
+                       const int32_t *order, int64_t n_pairs, int64_t pair_offset,
+                       const float *params, uint64_t seed, float *s_out, void *workspace,
+                       sg_stream_t stream);
+int32_t sg_fwd_bwd_src(const sg_model_t *model, const sg_pair_source_t *src,
+                       const int32_t *order, int64_t n_pairs, int64_t pair_offset,
+                       int64_t batch_total, const float *params, uint64_t seed,
+                       const float *y_stats, int32_t add_label_term, float *s_out,
+                       float *grad_out, float *loss_out, void *workspace, sg_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -90,3 +90,53 @@ def test_fast32_edge_cases(gpu):
                                      y_stats=batch.y_stats)
     model.fwd_bwd(empty, seed=1)
     assert float(model.grad.abs().max().item()) == 0.0
+
+
+def test_fast32_store_source_matches_records(gpu):
+    """Pairs gathered by the kernel from the dense graph store (sg_*_src, library 1.6)
+    == the same pairs packed into records, bit for bit: an explicit pair list and the
+    all-pairs grid, batch and class order; invalid graph ids raise the status word."""
+    import torch
+    from graphembedding_amd import _lib
+    from graphembedding_amd.packer import GraphStore
+    prob = small_problem(n_graphs=30, n_pairs=8, seed=29, n_lo=1, n_hi=30, n_max=30)
+    model, _ = prob.make_gpu_model(device=gpu)
+    assert model.kernel_path == 2
+    G, base, n = 30, 37, 700
+    q = np.arange(base, base + n)
+    pairs = np.stack([q // G, q % G], axis=1).astype(np.int32)
+    labels = np.random.default_rng(3).random(n).astype(np.float32)
+    store = GraphStore(prob.mgs, model.n_max, prob.d_in)
+    words = store.pack_host(pairs, labels, dtype='f32')
+    recs = torch.from_numpy(words.view(np.int32).reshape(-1)).to(gpu)
+    b_rec = model.batch_from_records(recs, n, labels, pair_offset=base)
+    pi = torch.from_numpy(pairs).to(gpu)
+    lab = torch.from_numpy(labels).to(gpu)
+    status = torch.zeros(1, dtype=torch.int32, device=gpu)
+    b_list = model.batch_from_store(store, n, lab, pair_idx=pi, pair_offset=base, status=status)
+    b_grid = model.batch_from_store(store, n, lab, grid_base=base, pair_offset=base,
+                                    status=status)
+    seed = 11
+
+    def run(b):
+        s = model.pred_sim_without_act(b, seed=seed).clone()
+        so = torch.empty(n, dtype=torch.float32, device=gpu)
+        model.fwd_bwd(b, seed=seed, s_out=so)
+        return s, so, model.grad.clone(), model.loss_buf.clone()
+
+    ref = run(b_rec)
+    for b in (b_list, b_grid):
+        for x, y in zip(ref, run(b)):
+            assert torch.equal(x, y)
+    model.balance(b_rec)
+    model.balance(b_grid)
+    assert torch.equal(b_rec.order, b_grid.order)
+    for x, y in zip(run(b_rec), run(b_grid)):
+        assert torch.equal(x, y)
+    assert int(status.item()) == 0
+    bad = pi.clone()
+    bad[5, 1] = G
+    b_bad = model.batch_from_store(store, n, lab, pair_idx=bad, pair_offset=base, status=status)
+    model.fwd_bwd(b_bad, seed=seed)
+    torch.cuda.synchronize()
+    assert int(status.item()) == _lib.SG_ERR_ARG

@@ -85,6 +85,29 @@ def test_validate_rejects_bad_models(L):
     assert path == 0
 
 
+def test_store_source_checks(L):
+    """sg_*_src argument checks (host side, before any launch): the store-sourced
+    entries serve the fused capacity-32 path only, and the store must match n_max."""
+    import torch
+    fake = torch.zeros(4, dtype=torch.int32)   # host tensors: only the pointers are read
+    dev = (fake, fake, fake)
+    m1 = _model(small_problem())                                   # path 1
+    with pytest.raises(_lib.SiameseHipError, match='SG_ERR_UNSUPPORTED'):
+        _lib.pair_order_src(m1, _lib.pair_source(dev, 10), 4, fake, fake, stream=0)
+    c4 = small_problem(n_graphs=6, n_pairs=4, n_lo=20, n_hi=30, n_max=30)
+    m2 = _lib.make_model(c4.layers, c4.d_in, 32, 0.9, c4.flags.final_act, c4.flags.sim_kernel,
+                         c4.flags.yeta)
+    assert _lib.validate(m2)[1] == 2
+    with pytest.raises(_lib.SiameseHipError, match='SG_ERR_ARG'):   # store n_max != 32
+        _lib.pair_order_src(m2, _lib.pair_source(dev, 30), 4, fake, fake, stream=0)
+    with pytest.raises(_lib.SiameseHipError, match='SG_ERR_ARG'):   # no store
+        _lib.forward_src(m2, _lib.SgPairSource(), 4, 0, fake, 1, fake, stream=0)
+    m3 = _lib.make_model(c4.layers, c4.d_in, 32, 0.9, c4.flags.final_act, c4.flags.sim_kernel,
+                         c4.flags.yeta, adj_dtype="bf16")
+    with pytest.raises(_lib.SiameseHipError, match='SG_ERR_UNSUPPORTED'):   # bf16 Â
+        _lib.pair_order_src(m3, _lib.pair_source(dev, 32), 4, fake, fake, stream=0)
+
+
 def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, 'LIB_PATH', str(tmp_path / 'nope.so'))
     monkeypatch.setattr(_lib, '_lib', None)
