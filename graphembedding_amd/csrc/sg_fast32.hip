@@ -51,6 +51,7 @@ constexpr int VS = 64;     // V[k][c] row stride (c < 2D)
 constexpr int NBUF = 80;   // NTN buffer floats per pair: x1[32] | x2[32] | gm[16]
 constexpr int MAXW = 8;    // waves per block (2 per SIMD)
 
+
 struct F32Args {
   const uint8_t *recs;
   const int32_t *order;
@@ -236,14 +237,28 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
   const int rw4h = A.rw4h;
   constexpr int ADJ4 = NC * NC / 4;   // 16-B words of a bf16 adjacency block
 
+  // The order entries of this wave's next 64 iterations (ordA) and the 64 after
+  // (ordB), one per lane, as vector loads: the next pair's id is known a whole pair
+  // ahead, with no scalar load that every LDS hand-off (lgkmcnt) would wait on.
+  auto load_ord = [&](int r0) -> int {
+    const int s_ = slot_of(r0 + l);
+    return s_ < npairs ? ord[s_] : 0;
+  };
+  auto ord_at = [&](int v, int lane) -> int {   // clamped: a bad order never reads out of bounds
+    const int x = __builtin_amdgcn_readlane(v, lane);
+    return x < 0 ? 0 : (x >= npairs ? npairs - 1 : x);
+  };
+  int ordA = 0, ordB = 0;
+  if (ord) {
+    ordA = load_ord(0);
+    ordB = load_ord(64);
+  }
+  int pnext = (ord && slot_of(0) < npairs) ? ord_at(ordA, 0) : slot_of(0);
+
   for (int it = 0;; ++it) {
     const int q = slot_of(it);
     if (q >= npairs) break;
-    int p = q;
-    if (ord) {
-      const int v = ord[q];
-      p = v < 0 ? 0 : (v >= npairs ? npairs - 1 : v);
-    }
+    const int p = pnext;
     // ---- stage the record (f32 LDS image; bf16 Â widened) ----
     {
       constexpr int NREC = (RW4 + 63) / 64;
@@ -314,6 +329,21 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
         }
       }
       sg_wsync();
+    }
+    // the next pair's id (an early L2 touch of its record measured 2% slower: the other
+    // wave of the SIMD already hides the record loads)
+    {
+      const int qn = slot_of(it + 1);
+      int pn = qn;
+      if (ord) {
+        const int rl = (it + 1) & 63;
+        if (rl == 0) {
+          ordA = ordB;
+          ordB = load_ord(it + 65);
+        }
+        pn = qn < npairs ? ord_at(ordA, rl) : 0;
+      }
+      pnext = pn;
     }
     const int *ty = (const int *)sRec + L::TAIL;
     int N0 = __builtin_amdgcn_readfirstlane(ty[2 * NC]);
