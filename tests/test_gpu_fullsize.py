@@ -26,15 +26,18 @@ def _spec(model, f):
                         weight_decay=f.weight_decay, dist_norm=f.dist_norm)
 
 
-def _graphs(gs):
-    return [O.Graph(adj=m.adj.astype(np.float32).astype(np.float64), types=m.types)
-            for m in gs.mgs]
+def _graphs(gs, bf16=False):
+    from graphembedding_amd.packer import bf16_round
+    # bf16 records hold Â rounded to bf16 (RNE); the kernels compute with that Â
+    cast = (lambda a: bf16_round(a.astype(np.float32))) if bf16 else \
+        (lambda a: a.astype(np.float32))
+    return [O.Graph(adj=cast(m.adj).astype(np.float64), types=m.types) for m in gs.mgs]
 
 
-def _oracle_scores(model, f, gs, pairs, keys, seed):
+def _oracle_scores(model, f, gs, pairs, keys, seed, bf16=False):
     spec = _spec(model, f)
     P = O.unflatten(spec, model.params.cpu().numpy().astype(np.float64))
-    og = _graphs(gs)
+    og = _graphs(gs, bf16)
     return np.array([O.pair_forward(spec, P, og[i], og[j], int(k), seed)[0]
                      for (i, j), k in zip(pairs, keys)])
 
@@ -75,6 +78,26 @@ def test_c2_full_allpairs_step(gpu):
         model.fwd_bwd(sh.batch(model), seed=seed, add_label_term=(r == 0))
         acc += model.grad_loss
     assert float((acc - g_full).abs().max().item()) <= 1e-5 * scale
+
+
+def test_c3_full_allpairs_bf16_sampled_pairs(gpu):
+    """C3: the C2 step with bf16 Â records (496 B/pair): sampled pairs vs the oracle on
+    the bf16-rounded Â."""
+    from graphembedding_amd.allpairs import AllPairsShard, load_graph_set
+    from graphembedding_amd.config import Flags
+    from graphembedding_amd.model_mse import SiameseGCNTNMSE
+    f = Flags(dropout=0.1, record_dtype='bf16')
+    gs = load_graph_set('syn_aids700nef', n_max=10)
+    labels = gs.label_matrix(f.yeta)
+    model = SiameseGCNTNMSE(gs.d_in, f, device=gpu, n_max=gs.n_max)
+    assert model.kernel_path == 1 and model.record_dtype == 'bf16'
+    batch = AllPairsShard(gs, labels, 0, 1, device=gpu, dtype='bf16').batch(model)
+    seed = 77
+    s = model.pred_sim_without_act(batch, seed=seed).cpu().numpy()
+    G = len(gs.graphs)
+    idx = np.random.default_rng(13).choice(batch.n_pairs, 48, replace=False)
+    ref = _oracle_scores(model, f, gs, [(i // G, i % G) for i in idx], idx, seed, bf16=True)
+    np.testing.assert_allclose(s[idx], ref, rtol=TOL, atol=TOL)
 
 
 def test_c4_full_grid_sampled_pairs(gpu):
