@@ -97,9 +97,18 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    # SG_BENCH_REHEARSAL=1 (diagnostic): every rank on cuda:0 over gloo, to rehearse the
+    # multi-rank path (shards, all-reduce hook, barriers, max-over-ranks timing) on a
+    # one-GPU box; its numbers are not a scaling measurement
+    rehearsal = os.environ.get('SG_BENCH_REHEARSAL') == '1'
+    if rehearsal:
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if rehearsal:
+            dist.init_process_group('gloo')
+        else:
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
     device = torch.device('cuda', local)
 
     from graphembedding_amd import _lib
