@@ -23,9 +23,11 @@ def _stale() -> bool:
     return any(os.path.isfile(d) and os.path.getmtime(d) > t for d in deps)
 
 
-# per-source compiler options: the fused AIDS700nef kernel schedules for ILP (max-ilp:
-# +1.2% measured; the capacity-32 kernel measured 0.8% slower with it)
-SOURCE_FLAGS = {'sg_fast.hip': ['-mllvm', '-amdgpu-sched-strategy=max-ilp']}
+# per-source compiler options (A/B-measured): the fused AIDS700nef kernel schedules for
+# ILP (max-ilp: +1.2%; the capacity-32 kernel measured 0.8% slower with it), the
+# capacity-32 kernel with the AMDGPU register-pressure trackers (+0.5%)
+SOURCE_FLAGS = {'sg_fast.hip': ['-mllvm', '-amdgpu-sched-strategy=max-ilp'],
+                'sg_fast32.hip': ['-mllvm', '-amdgpu-use-amdgpu-trackers']}
 
 
 def build_hip(force: bool = False, verbose: bool = False, out: str = None, defines=()) -> str:
