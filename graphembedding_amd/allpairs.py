@@ -133,8 +133,9 @@ class AllPairsStream(object):
     chunk order (deterministic), leaving model.grad / model.loss_buf as one fwd_bwd
     over the whole shard would (up to fp32 summation order).
 
-    source='auto' skips the records when the model runs the fused capacity-32 kernel
-    with f32 Â (config C4): the kernel then gathers every pair's graphs from the store
+    source='auto' skips the records when the model runs a fused kernel with f32 Â
+    (config C4's capacity-32 one in particular): the kernel then gathers every pair's
+    graphs from the store
     (sg_fwd_bwd_src, library 1.6) and the pack pass with its 8.5 KB-per-pair write and
     read-back disappears.  source='records' always packs.
     """
@@ -173,7 +174,7 @@ class AllPairsStream(object):
             yield c0, min(self.chunk, self.end - c0)
 
     def uses_store(self, model) -> bool:
-        return (self.source == 'auto' and model.kernel_path == 2 and self.dtype == 'f32' and
+        return (self.source == 'auto' and model.kernel_path in (1, 2) and self.dtype == 'f32' and
                 model.record_dtype == 'f32' and self.store.n_max == model.n_max)
 
     def _pack(self, model, c0: int, n: int):

@@ -75,7 +75,60 @@ struct FastArgs {
   int d_in, n_params;
   int shared_floats, wave_floats;
   int oW0, ob0, oW1, ob1, oWd, obd, oW, oV, oU, obn;
+  // pair source (sg_pair_source_t): src_store = 1 gathers each record from the dense
+  // graph store instead of reading a packed one
+  int src_store, G;
+  const float *sadj;
+  const int32_t *stypes, *sn, *spairs;
+  int64_t grid_base;
+  const float *slabels;
+  int32_t *status;
 };
+
+// 16-B word w4 of pair p's f32 record (sg_rec_layout(D): Â of both sides, types of
+// both sides, n0, n1, label, tag) gathered from the dense store, one dword at a time
+// (the store rows are D·D and D words: no 16-B alignment to rely on).  Invalid graph
+// ids read as a zero record and raise *status, as sg_pack_pairs does.
+template <int D>
+__device__ __forceinline__ uint4 fast_store_word(const FastArgs &A, int p, int w4, int lane) {
+  int g0, g1;
+  if (A.spairs) {
+    g0 = A.spairs[2 * (int64_t)p];
+    g1 = A.spairs[2 * (int64_t)p + 1];
+  } else {
+    const int64_t q = A.grid_base + p;
+    g0 = (int)(q / A.G);
+    g1 = (int)(q - (int64_t)g0 * A.G);
+  }
+  const bool ok = (unsigned)g0 < (unsigned)A.G && (unsigned)g1 < (unsigned)A.G;
+  if (!ok && lane == 0 && A.status) atomicExch(A.status, (int32_t)SG_ERR_ARG);
+  constexpr int NN = D * D;
+  uint32_t v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int w = 4 * w4 + k;
+    uint32_t x = 0u;
+    if (ok) {
+      if (w < 2 * NN) {
+        const int s = w >= NN;
+        x = __float_as_uint(A.sadj[(size_t)(s ? g1 : g0) * NN + (w - s * NN)]);
+      } else if (w < 2 * NN + 2 * D) {
+        const int t = w - 2 * NN, s = t >= D;
+        x = (uint32_t)A.stypes[(size_t)(s ? g1 : g0) * D + (t - s * D)];
+      } else if (w == 2 * NN + 2 * D) {
+        x = (uint32_t)A.sn[g0];
+      } else if (w == 2 * NN + 2 * D + 1) {
+        x = (uint32_t)A.sn[g1];
+      } else if (w == 2 * NN + 2 * D + 2) {
+        x = __float_as_uint(A.slabels ? A.slabels[p] : 0.f);
+      } else if (w == 2 * NN + 2 * D + 3) {
+        x = (uint32_t)p;
+      }
+    }
+    v[k] = x;
+  }
+  return uint4{v[0], v[1], v[2], v[3]};
+}
 
 template <int D, bool AVG = false>
 struct FastLds {
@@ -156,7 +209,7 @@ __device__ unsigned long long sg_fast_times[kTimeWaves * 5];
 #define SG_STAMP(slot, val) do {} while (0)
 #endif
 
-template <int D, bool BWD, bool ALIGNED, bool INTENDED, bool AVG>
+template <int D, bool BWD, bool ALIGNED, bool INTENDED, bool AVG, bool SRC>
 __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   SG_STAMP(0, __builtin_amdgcn_s_memrealtime());
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -257,7 +310,8 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   for (int c = 0; c < NREC; ++c) {
     const int w4 = l + 64 * c;
     pre[c] = (q < npairs && w4 < rw4h)
-                 ? ((const uint4 *)(A.recs + (size_t)p * (size_t)rw4h * 16u))[w4]
+                 ? (SRC ? fast_store_word<D>(A, p, w4, l)
+                                : ((const uint4 *)(A.recs + (size_t)p * (size_t)rw4h * 16u))[w4])
                  : uint4{0u, 0u, 0u, 0u};
   }
   __syncthreads();
@@ -417,7 +471,9 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       for (int c = 0; c < NREC; ++c) {
         const int w4 = l + 64 * c;
         if (qn < npairs && w4 < rw4h)
-          pre[c] = ((const uint4 *)(A.recs + (size_t)pn * (size_t)rw4h * 16u))[w4];
+          pre[c] = SRC
+                       ? fast_store_word<D>(A, pn, w4, l)
+                       : ((const uint4 *)(A.recs + (size_t)pn * (size_t)rw4h * 16u))[w4];
       }
       q = qn;
       p = pn;
@@ -1063,28 +1119,37 @@ int64_t sg_fast_slab_floats(const SgGenPlan &P, int64_t n_pairs) {
   return (int64_t)c.blocks * (P.n_params + 1);
 }
 
-template <int D, bool BWD, bool ALIGNED, bool INTENDED, bool AVG>
+template <int D, bool BWD, bool ALIGNED, bool INTENDED, bool AVG, bool SRC>
 static void launch_one(const FastCfg &c, const FastArgs &A, hipStream_t st) {
-  const void *fn = (const void *)sg_fast_kernel<D, BWD, ALIGNED, INTENDED, AVG>;
+  const void *fn = (const void *)sg_fast_kernel<D, BWD, ALIGNED, INTENDED, AVG, SRC>;
   if (c.lds > 65536u)
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds);
-  hipLaunchKernelGGL((sg_fast_kernel<D, BWD, ALIGNED, INTENDED, AVG>), dim3(c.blocks),
+  hipLaunchKernelGGL((sg_fast_kernel<D, BWD, ALIGNED, INTENDED, AVG, SRC>), dim3(c.blocks),
                      dim3(64 * c.waves), c.lds, st, A);
 }
 
+template <int D, bool AVG, bool SRC>
+static void launch_fast_src(const FastCfg &c, bool bwd, bool aligned, bool intended,
+                            const FastArgs &A, hipStream_t st) {
+  if (!bwd) {
+    if (intended) launch_one<D, false, false, true, AVG, SRC>(c, A, st);
+    else launch_one<D, false, false, false, AVG, SRC>(c, A, st);
+  } else if (aligned) {
+    if (intended) launch_one<D, true, true, true, AVG, SRC>(c, A, st);
+    else launch_one<D, true, true, false, AVG, SRC>(c, A, st);
+  } else {
+    if (intended) launch_one<D, true, false, true, AVG, SRC>(c, A, st);
+    else launch_one<D, true, false, false, AVG, SRC>(c, A, st);
+  }
+}
+
+// SRC: store-sourced pairs (a separate instantiation: the gather's registers would
+// otherwise cost the record path spills)
 template <int D, bool AVG>
 static void launch_fast(const FastCfg &c, bool bwd, bool aligned, bool intended,
                         const FastArgs &A, hipStream_t st) {
-  if (!bwd) {
-    if (intended) launch_one<D, false, false, true, AVG>(c, A, st);
-    else launch_one<D, false, false, false, AVG>(c, A, st);
-  } else if (aligned) {
-    if (intended) launch_one<D, true, true, true, AVG>(c, A, st);
-    else launch_one<D, true, true, false, AVG>(c, A, st);
-  } else {
-    if (intended) launch_one<D, true, false, true, AVG>(c, A, st);
-    else launch_one<D, true, false, false, AVG>(c, A, st);
-  }
+  if (A.src_store) launch_fast_src<D, AVG, true>(c, bwd, aligned, intended, A, st);
+  else launch_fast_src<D, AVG, false>(c, bwd, aligned, intended, A, st);
 }
 
 int sg_ntn_wgrad_run(const float *ntn, int64_t n_pairs, int D, int oW, int oV, int obn, int C,
@@ -1095,13 +1160,25 @@ int sg_fast_needs_ntn(const SgGenPlan &P) { return plan_avg(P) ? 1 : 0; }
 int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
                 const int32_t *order, int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
                 uint64_t seed, const float *y_stats, float *s_out, float *slab, float *ntn,
-                int *blocks_out, hipStream_t stream, const uint64_t *seed_dev) {
+                int *blocks_out, hipStream_t stream, const uint64_t *seed_dev,
+                const sg_pair_source_t *src) {
   const int D = P.n_max;
   FastCfg c = fast_cfg(P, n_pairs, bwd);
   // the kernel indexes pairs in 32 bits (2^31 records would be ≥ 1 TB)
   if (n_pairs > 0x7FFFFFFF - (int64_t)c.blocks * c.waves * 2) return SG_ERR_ARG;
   FastArgs A;
   A.recs = (const uint8_t *)recs;
+  A.src_store = src ? 1 : 0;
+  A.G = src ? src->n_graphs : 0;
+  A.sadj = src ? src->adj : nullptr;
+  A.stypes = src ? src->types : nullptr;
+  A.sn = src ? src->n : nullptr;
+  A.spairs = src ? src->pair_idx : nullptr;
+  A.grid_base = src ? src->grid_base : 0;
+  A.slabels = src ? src->labels : nullptr;
+  A.status = src ? src->status : nullptr;
+  if (src && (P.adj_dtype != SG_DTYPE_F32 || src->n_max != D || src->n_graphs <= 0))
+    return SG_ERR_ARG;
   A.order = order;
   A.n_pairs = n_pairs;
   A.rw4h = P.hbm_words / 4;

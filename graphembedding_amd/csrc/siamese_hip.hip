@@ -36,7 +36,8 @@ int sg_fast_needs_ntn(const SgGenPlan &P);
 int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
                 const int32_t *order, int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
                 uint64_t seed, const float *y_stats, float *s_out, float *slab, float *ntn,
-                int *blocks_out, hipStream_t stream, const uint64_t *seed_dev = nullptr);
+                int *blocks_out, hipStream_t stream, const uint64_t *seed_dev = nullptr,
+                const sg_pair_source_t *src = nullptr);
 // fused capacity-32 path (sg_fast32.hip)
 int sg_fast32_supported(const sg_model_t *m, const SgGenPlan &P);
 // graph-store path for Web-sized graphs (sg_web.hip)
@@ -615,7 +616,7 @@ int32_t sg_pair_order(const sg_model_t *model, const void *records, int64_t n_pa
 // a store-sourced call's checks: fused capacity-32 path, f32 Â, store shape = n_max
 static int32_t src_check(const PathChoice &c, const sg_pair_source_t *src) {
   if (!src || !src->adj || !src->types || !src->n || src->n_graphs <= 0) return SG_ERR_ARG;
-  if (c.path != 2 || c.plan.adj_dtype != SG_DTYPE_F32) return SG_ERR_UNSUPPORTED;
+  if ((c.path != 1 && c.path != 2) || c.plan.adj_dtype != SG_DTYPE_F32) return SG_ERR_UNSUPPORTED;
   if (src->n_max != c.plan.n_max || src->grid_base < 0) return SG_ERR_ARG;
   return SG_OK;
 }
@@ -704,7 +705,7 @@ static int32_t fwd_bwd_impl(const sg_model_t *model, const void *records, const 
   if (c.path == 1)
     rc = sg_fast_run(model, c.plan, true, records, order, n_pairs, pair_offset, batch_total,
                      params, seed, y_stats, s_out, slab, slab + ntn_offset_floats(c, n_pairs),
-                     &nblk, st, seed_dev);
+                     &nblk, st, seed_dev, src);
   else if (c.path == 2)
     rc = sg_fast32_run(model, c.plan, true, records, order, n_pairs, pair_offset, batch_total,
                        params, seed, y_stats, s_out, slab, slab + ntn_offset_floats(c, n_pairs),
@@ -752,6 +753,10 @@ int32_t sg_forward_src(const sg_model_t *model, const sg_pair_source_t *src,
   if (rc != SG_OK) return rc;
   if (n_pairs == 0) return SG_OK;
   if (!params || !s_out) return SG_ERR_ARG;
+  if (c.path == 1)
+    return sg_fast_run(model, c.plan, false, nullptr, order, n_pairs, pair_offset, n_pairs, params,
+                       seed, nullptr, s_out, nullptr, nullptr, nullptr, (hipStream_t)stream,
+                       nullptr, src);
   return sg_fast32_run(model, c.plan, false, nullptr, order, n_pairs, pair_offset, n_pairs, params,
                        seed, nullptr, s_out, nullptr, nullptr, nullptr, (hipStream_t)stream, src);
 }

@@ -281,14 +281,13 @@ class SiameseGCNTNMSE(object):
     def batch_from_store(self, store, n_pairs, labels, pair_idx=None, grid_base=0,
                          pair_offset=0, batch_total=None, y_stats=None, status=None) -> Batch:
         """A batch whose pairs the fused kernel gathers from the dense store itself
-        (sg_*_src, library 1.6; kernel path 2 with f32 Â): store = packer.GraphStore,
+        (sg_*_src, library 1.6; kernel paths 1 and 2 with f32 Â): store = packer.GraphStore,
         pair_idx int32 [n, 2] device tensor or None for the all-pairs grid (pair i =
         divmod(grid_base + i, G)), labels float32 [n] device tensor.  Same results as
         packing the pairs into records (sg_pack_pairs) and stepping those."""
-        if self.kernel_path != 2 or self.record_dtype != 'f32':
-            raise _lib.SiameseHipError('store-sourced batches need the fused capacity-32 '
-                                       'path with f32 records (kernel path {})'.format(
-                                           self.kernel_path))
+        if self.kernel_path not in (1, 2) or self.record_dtype != 'f32':
+            raise _lib.SiameseHipError('store-sourced batches need a fused kernel path with '
+                                       'f32 records (kernel path {})'.format(self.kernel_path))
         if store.n_max != self.n_max:
             raise _lib.SiameseHipError('store n_max {} != model n_max {}'.format(store.n_max,
                                                                                  self.n_max))

@@ -383,8 +383,8 @@ int32_t sg_adam_tf_ex(float *params, float *m, float *v, const float *grad, int6
  *   labels    [n_pairs] f32 or NULL (label := 0);
  *   status    device int or NULL: invalid graph ids set SG_ERR_ARG and read as a
  *             zero record, as in sg_pack_pairs.
- * Fused capacity-32 path (sg_model_validate path 2) with f32 Â only; other models
- * give SG_ERR_UNSUPPORTED.  Workspace sizes are sg_workspace_bytes /
+ * Fused paths (sg_model_validate paths 1 and 2) with f32 Â only; other models give
+ * SG_ERR_UNSUPPORTED.  Workspace sizes are sg_workspace_bytes /
  * sg_pair_order_workspace_bytes.
  */
 typedef struct sg_pair_source {

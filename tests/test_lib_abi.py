@@ -87,13 +87,18 @@ def test_validate_rejects_bad_models(L):
 
 def test_store_source_checks(L):
     """sg_*_src argument checks (host side, before any launch): the store-sourced
-    entries serve the fused capacity-32 path only, and the store must match n_max."""
+    entries serve the fused paths only, and the store must match n_max."""
     import torch
     fake = torch.zeros(4, dtype=torch.int32)   # host tensors: only the pointers are read
     dev = (fake, fake, fake)
-    m1 = _model(small_problem())                                   # path 1
+    att = small_problem(flags_overrides=dict(AVERAGE_STACK, layer_2='Attention:input_dim=16'))
+    m0 = _model(att)                                               # generic path 0
+    assert _lib.validate(m0)[1] == 0
     with pytest.raises(_lib.SiameseHipError, match='SG_ERR_UNSUPPORTED'):
-        _lib.pair_order_src(m1, _lib.pair_source(dev, 10), 4, fake, fake, stream=0)
+        _lib.pair_order_src(m0, _lib.pair_source(dev, 10), 4, fake, fake, stream=0)
+    m1 = _model(small_problem())                                   # path 1, store n_max 12
+    with pytest.raises(_lib.SiameseHipError, match='SG_ERR_ARG'):
+        _lib.pair_order_src(m1, _lib.pair_source(dev, 12), 4, fake, fake, stream=0)
     c4 = small_problem(n_graphs=6, n_pairs=4, n_lo=20, n_hi=30, n_max=30)
     m2 = _lib.make_model(c4.layers, c4.d_in, 32, 0.9, c4.flags.final_act, c4.flags.sim_kernel,
                          c4.flags.yeta)
