@@ -48,9 +48,10 @@ def parse():
                    help='record processing order: class-balanced (sg_pair_order) or batch order')
     p.add_argument('--chunk', type=int, default=4_000_000,
                    help='C4: pairs per packed chunk when a shard does not fit HBM')
-    p.add_argument('--source', choices=('auto', 'records'), default='auto',
+    p.add_argument('--source', choices=('auto', 'records', 'store'), default='auto',
                    help='C4 streamed: the kernel gathers pairs from the graph store (auto) or '
-                        'packs records per chunk (records)')
+                        'packs records per chunk (records); store: also the resident '
+                        'C2/C3 shard (diagnostic, no records at all)')
     p.add_argument('--store-chunk', type=int, default=25_000_000,
                    help='C4 streamed from the store: pairs per launch')
     p.add_argument('--resident-gb', type=float, default=150.0,
@@ -155,11 +156,17 @@ def main():
         store_src = args.source == 'auto' and model.kernel_path == 2 and args.records == 'f32'
         shard = AllPairsStream(gs, labels, srank, sworld, device=device,
                                chunk=args.store_chunk if store_src else args.chunk,
-                               dtype=args.records, balance=balance, source=args.source)
+                               dtype=args.records, balance=balance,
+                               source='records' if args.source == 'records' else 'auto')
         batch = None
     if not web and not streamed:
         shard = AllPairsShard(gs, labels, srank, sworld, device=device, dtype=args.records)
         batch = shard.batch(model, balance=balance)
+        if args.source == 'store':   # same pairs, gathered by the kernel from the store
+            batch = model.batch_from_store(gs.store, shard.n, batch.labels,
+                                           grid_base=shard.start, pair_offset=shard.start,
+                                           batch_total=shard.total, y_stats=batch.y_stats)
+            batch = model.balance(batch) if balance else batch
     hook = make_allreduce_hook() if world > 1 else None
     if not web:
         model.workspace(shard.chunk if streamed else batch.n_pairs)
