@@ -291,6 +291,17 @@ class SiameseGCNTNMSE(object):
         if store.n_max != self.n_max:
             raise _lib.SiameseHipError('store n_max {} != model n_max {}'.format(store.n_max,
                                                                                  self.n_max))
+        torch = self.torch
+        n_pairs = int(n_pairs)
+        # the kernel reads pair_idx[0 .. 2n) and labels[0 .. n): check before it does
+        if pair_idx is not None:
+            if (not torch.is_tensor(pair_idx) or pair_idx.dtype != torch.int32 or
+                    not pair_idx.is_contiguous() or pair_idx.numel() < 2 * n_pairs):
+                raise _lib.SiameseHipError('pair_idx must be a contiguous int32 [n, 2] tensor')
+        elif int(grid_base) < 0:
+            raise _lib.SiameseHipError('grid_base must be >= 0')
+        if torch.is_tensor(labels) and labels.numel() < n_pairs:
+            raise _lib.SiameseHipError('labels has fewer than n_pairs entries')
         dev = store.to_device(self.device)
         b = self.batch_from_records(None, n_pairs, labels, pair_offset=pair_offset,
                                     batch_total=batch_total, y_stats=y_stats)

@@ -52,3 +52,25 @@ def test_pair_source_struct(gs):
     assert src.labels == lab.data_ptr() and not src.status
     grid = _lib.pair_source((adj, types, n), 32)
     assert not grid.pair_idx and grid.grid_base == 0
+
+
+def test_batch_from_store_checks(gs):
+    """Bad pair lists are refused on the host (the kernel would read past them)."""
+    from graphembedding_amd.config import Flags
+    from graphembedding_amd.model_mse import SiameseGCNTNMSE
+    f = Flags(dropout=0.1, layer_3='Padding:max_in_dims=30,padding_value=0',
+              layer_4='NTN:input_dim=30,feature_map_dim=10,inneract=relu,dropout=True,'
+                      'bias=True')
+    model = SiameseGCNTNMSE(gs.d_in, f, device='cpu', n_max=32)
+    assert model.kernel_path == 2
+    lab = torch.zeros(8)
+    with pytest.raises(_lib.SiameseHipError):
+        model.batch_from_store(gs.store, 8, lab, pair_idx=torch.zeros((4, 2), dtype=torch.int32))
+    with pytest.raises(_lib.SiameseHipError):
+        model.batch_from_store(gs.store, 8, lab, pair_idx=torch.zeros((8, 2)))
+    with pytest.raises(_lib.SiameseHipError):
+        model.batch_from_store(gs.store, 8, torch.zeros(3), grid_base=0)
+    with pytest.raises(_lib.SiameseHipError):
+        model.batch_from_store(gs.store, 8, lab, grid_base=-1)
+    b = model.batch_from_store(gs.store, 8, lab, grid_base=3, pair_offset=3)
+    assert b.records is None and b.src.grid_base == 3 and b.n_pairs == 8
