@@ -265,6 +265,11 @@ class SiameseGCNTNMSE(object):
     def batch_from_records(self, recs, n_pairs, labels, pair_offset=0, batch_total=None,
                            gid_pairs=None, y_stats=None) -> Batch:
         torch = self.torch
+        if recs is not None:   # the kernels read n_pairs whole records
+            need = int(n_pairs) * record_words(self.n_max, self.record_dtype)
+            if recs.numel() * recs.element_size() < 4 * need:
+                raise _lib.SiameseHipError('records hold fewer than n_pairs = {} records of '
+                                           '{} B'.format(int(n_pairs), 4 * need // max(1, int(n_pairs))))
         lab = torch.as_tensor(np.asarray(labels, np.float32) if not torch.is_tensor(labels)
                               else labels, dtype=torch.float32, device=self.device)
         if y_stats is None:
