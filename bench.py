@@ -13,8 +13,8 @@ pair shard, deterministic gradient reduction, RCCL all-reduce of the flat
 gradient (N > 1), TF-form Adam.  Inputs (packed pair records) are resident in
 HBM before timing starts.  Prints ONE JSON line (rank 0).
 
-  python bench.py [--gpus N --steps K --warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...
+  python bench.py [--gpus N --steps K --warmup W]   (N > 1: starts N ranks itself)
+  torchrun --nproc-per-node N bench.py --gpus N ...  (--gpus must equal WORLD_SIZE)
 """
 from __future__ import annotations
 
@@ -84,8 +84,32 @@ def cpu_baseline(gs, labels, flags, n_sample, D=None):
     return out
 
 
+def launch_ranks(args) -> int:
+    """`python bench.py --gpus N` without a torchrun environment: start the N ranks as
+    children under torch.distributed.run (one process per GPU, 127.0.0.1 rendezvous)
+    before this process touches the GPU, and return their exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node={}'.format(args.gpus), '--master-addr=127.0.0.1',
+           '--master-port={}'.format(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    env_world = os.environ.get('WORLD_SIZE')
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    if env_world is not None and int(env_world) != args.gpus and \
+            os.environ.get('SG_BENCH_REHEARSAL') != '1':
+        sys.exit('bench.py: --gpus {} but WORLD_SIZE={} (launch one rank per GPU)'.format(
+            args.gpus, env_world))
+    if args.gpus < 1:
+        sys.exit('bench.py: --gpus must be >= 1')
     web = args.dataset == 'syn_web'
     if args.steps is None:
         args.steps = 3 if web else 50

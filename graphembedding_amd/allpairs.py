@@ -113,8 +113,10 @@ class AllPairsShard(object):
                                     device=device)
         self.n = self.end - self.start
         self.record_bytes = 4 * record_words(gs.n_max, dtype)
+        self.store_n = gs.store.n
 
     def batch(self, model, rank: int = 0, balance: bool = True):
+        model.check_node_counts(self.store_n, 'AllPairsShard')
         b = model.batch_from_records(self.records, self.n, self.labels,
                                      pair_offset=self.start, batch_total=self.total,
                                      y_stats=self.y_stats)
@@ -179,6 +181,7 @@ class AllPairsStream(object):
 
     def _pack(self, model, c0: int, n: int):
         torch = self.torch
+        model.check_node_counts(self.store.n, 'AllPairsStream')
         lab = self.labels[c0 - self.start:c0 - self.start + n]
         if self.uses_store(model):
             b = model.batch_from_store(self.store, n, lab, grid_base=c0, pair_offset=c0,

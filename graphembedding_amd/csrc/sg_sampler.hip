@@ -72,12 +72,13 @@ __global__ void __launch_bounds__(1024) sg_feed_kernel(sg_feed_t F, int32_t *__r
                                                       int32_t *__restrict__ status) {
   const int t = threadIdx.x;
   const int B = F.batch;
-  const int count = F.compat ? B + B * B : B;
+  // B + B² sampler calls in 'compat' mode: int64 (B >= 46,341 would overflow int)
+  const int64_t count = F.compat ? (int64_t)B + (int64_t)B * B : (int64_t)B;
   if (F.kind == 0) {   // RandomSampler (samplers.py:24-31)
     int32_t *st = F.state, *L = st + 1, *tmp = st + 1 + F.n;
     int idx = st[0];
     if (idx < 0 || idx >= F.n) idx = 0;
-    for (int c = 0; c < count; ++c) {
+    for (int64_t c = 0; c < count; ++c) {
       const int g1 = L[idx];
       ++idx;
       if (idx >= F.n) {
@@ -97,7 +98,7 @@ __global__ void __launch_bounds__(1024) sg_feed_kernel(sg_feed_t F, int32_t *__r
     if (t == 0) st[0] = idx;
   } else if (t == 0) {   // DistributionSampler (samplers.py:51-68)
     int cur = F.state[0], item = F.state[1];
-    for (int c = 0; c < count; ++c) {
+    for (int64_t c = 0; c < count; ++c) {
       pairs[2 * c] = F.dens_order[F.bins[cur] * F.bin_size + item];
       pairs[2 * c + 1] = F.dens_order[F.bins[cur + 1] * F.bin_size + item];
       cur += 2;
@@ -109,11 +110,11 @@ __global__ void __launch_bounds__(1024) sg_feed_kernel(sg_feed_t F, int32_t *__r
   }
   __syncthreads();
   // labels: of the input pairs, or (quirk A3) of the last B calls
-  if (t < B) {
-    const int c = F.compat ? count - B + t : t;
+  for (int i = t; i < B; i += blockDim.x) {   // any B, not just one per thread
+    const int64_t c = F.compat ? count - B + i : i;
     const int a = pairs[2 * c], b = pairs[2 * c + 1];
     const bool ok = a >= 0 && a < F.label_n && b >= 0 && b < F.label_n;
-    labels[t] = ok ? F.label_matrix[(size_t)a * F.label_n + b] : 0.f;
+    labels[i] = ok ? F.label_matrix[(size_t)a * F.label_n + b] : 0.f;
   }
   __syncthreads();
   if (t == 0) {   // ȳ and ½Σ(y - ȳ)² in double, in order

@@ -148,6 +148,7 @@ class DeviceFeed(object):
         self.sampler = device_sampler(coll.sampler, model.device)
         gl = self.sampler.gs
         self.store = GraphStore(gl, model.n_max, model.input_dim)
+        model.check_node_counts(self.store.n, 'DeviceFeed')
         Y = labels if labels is not None else label_matrix(model, gl, dist_calculator, data)
         self.Y = torch.from_numpy(np.ascontiguousarray(Y, dtype=np.float32)).to(model.device)
         B = model.flags.batch_size

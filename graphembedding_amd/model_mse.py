@@ -93,9 +93,10 @@ class SiameseGCNTNMSE(object):
         self.layers = create_layers(f, self.input_dim)
         pd = padding_dims(self.layers)
         self.n_max = int(n_max or f.n_max or pd or 10)
-        if pd is not None and self.n_max > pd:
-            # records may hold up to n_max nodes; the reference's tf.pad requires N <= pd
-            pass
+        # the reference's tf.pad fails for N > max_in_dims (layers.py:226, quirk A9); the
+        # kernels would drop the extra nodes instead, so every store is checked on entry
+        # (check_node_counts) even when the record capacity n_max exceeds the Padding dim
+        self.max_nodes = pd
         self.sim_kernel = create_sim_kernel(f.sim_kernel, f.yeta)
         self.final_act_np = create_activation(f.final_act, self.sim_kernel)
         self.record_dtype = getattr(f, 'record_dtype', 'f32') or 'f32'
@@ -148,6 +149,16 @@ class SiameseGCNTNMSE(object):
     def is_web(self) -> bool:
         """Graph-store path (sg_web_*, config C5): Padding/NTN width in [32, 512]."""
         return self.kernel_path == _lib.PATH_WEB
+
+    def check_node_counts(self, n_nodes, what='graph store'):
+        """Raise like the reference's tf.pad (layers.py:226, quirk A9) when a graph has
+        more nodes than the Padding layer's max_in_dims."""
+        n = np.asarray(n_nodes).reshape(-1)
+        if self.max_nodes is not None and n.size and int(n.max()) > self.max_nodes:
+            k = int(np.argmax(n))
+            raise _lib.SiameseHipError(
+                '{}: graph {} has {} nodes > Padding max_in_dims {} (layers.py:226)'.format(
+                    what, k, int(n[k]), self.max_nodes))
 
     # ---- reference API ------------------------------------------------------
     def apply_final_act_np(self, score):
@@ -215,6 +226,7 @@ class SiameseGCNTNMSE(object):
                     uniq.append(g)
                 idx[k, c] = index[id(g)]
         store = GraphStore(uniq, self.n_max, self.input_dim)
+        self.check_node_counts(store.n, 'make_batch')
         lab = np.zeros(len(g1s), np.float32) if labels is None else np.asarray(labels, np.float32)
         words = store.pack_host(idx, lab, dtype=self.record_dtype)
         recs = torch.from_numpy(words.view(np.int32).reshape(-1)).to(self.device)
@@ -247,6 +259,7 @@ class SiameseGCNTNMSE(object):
     def web_batch(self, store, pairs, labels, pair_offset=0, batch_total=None, y_stats=None,
                   chunk=None) -> Batch:
         n = int(pairs.shape[0])
+        self.check_node_counts(store.n, 'web_batch')
         b = self.batch_from_records(None, n, labels, pair_offset, batch_total, y_stats=y_stats)
         b.csr, b.pairs = store, pairs
         b.chunk = int(chunk or min(max(n, 1), 32768))
@@ -298,6 +311,7 @@ class SiameseGCNTNMSE(object):
                                                                                  self.n_max))
         torch = self.torch
         n_pairs = int(n_pairs)
+        self.check_node_counts(store.n, 'batch_from_store')
         # the kernel reads pair_idx[0 .. 2n) and labels[0 .. n): check before it does
         if pair_idx is not None:
             if (not torch.is_tensor(pair_idx) or pair_idx.dtype != torch.int32 or
@@ -399,10 +413,27 @@ class SiameseGCNTNMSE(object):
         the captured steps; fused path (default / Average stack) only."""
         return GraphSteps(self, feed, n_steps)
 
+    # validation draws its dropout masks from a stream of its own: the reference's val
+    # sess.run (train.py:19-21) samples independently of the train steps
+    VAL_SEED_STREAM = 1 << 62
+
+    def val_seed(self, seed=None):
+        """An explicit seed is used as given; the default is the step's seed moved to the
+        validation stream."""
+        if seed is not None:
+            return int(seed)
+        return (self._seed(None) ^ self.VAL_SEED_STREAM) & 0xFFFFFFFFFFFFFFFF
+
     def val_loss(self, batch: Batch, seed=None):
-        self.fwd_bwd(batch, seed)
+        """sess.run([merged, loss]) on valid_data (train.py:19-21): the loss at the current
+        parameters, with independent dropout masks (val_seed); self.grad / loss_buf keep
+        the last training step's values."""
+        saved = self.grad_loss.clone()
+        self.fwd_bwd(batch, self.val_seed(seed))
+        loss = float(self.loss_buf[0].item())
+        self.grad_loss.copy_(saved)
         reg = self.flags.weight_decay * 0.5 * float((self.params.double() ** 2).sum().item())
-        return float(self.loss_buf[0].item()) + reg
+        return loss + reg
 
     def test_scores(self, batch: Batch, seed=None):
         return self.pred_sim_without_act(batch, seed).cpu().numpy().astype(np.float64)

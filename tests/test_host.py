@@ -177,3 +177,39 @@ def test_label_matrix_matrix_path_equals_lookup_path():
     del dc.matrix
     slow = label_matrix(_M, gl, dc, data)
     assert fast.dtype == np.float32 and np.array_equal(fast, slow)
+
+
+def test_graph_larger_than_padding_dim_is_refused():
+    """tf.pad fails for N > max_in_dims (layers.py:226, quirk A9): the host refuses such
+    a graph even when the record capacity (32) exceeds the Padding dim (30), instead of
+    letting the kernels drop the extra nodes."""
+    import torch
+    from graphembedding_amd import _lib
+    from graphembedding_amd.model_mse import SiameseGCNTNMSE
+    prob = small_problem(n_graphs=4, n_pairs=3, seed=2, n_lo=29, n_hi=31, n_max=30)
+    sizes = [m.num_nodes() for m in prob.mgs]
+    model = SiameseGCNTNMSE(prob.d_in, prob.flags, device='cpu', n_max=32, params=prob.params)
+    assert model.n_max == 32 and model.max_nodes == 30
+    big = [m for m in prob.mgs if m.num_nodes() > 30]
+    ok = [m for m in prob.mgs if m.num_nodes() <= 30]
+    assert big and ok, sizes
+    with pytest.raises(_lib.SiameseHipError, match='max_in_dims 30'):
+        model.make_batch([ok[0], big[0]], [ok[0], ok[0]])
+    with pytest.raises(_lib.SiameseHipError, match='max_in_dims 30'):
+        model.batch_from_store(GraphStore(prob.mgs, 32, prob.d_in), 2, torch.zeros(2),
+                               grid_base=0)
+    b = model.make_batch([ok[0]], [ok[-1]])
+    assert b.n_pairs == 1
+
+
+def test_validation_seed_stream_is_distinct():
+    """val_loss draws dropout masks independently of the train steps: its
+    default seed is never a train-step seed."""
+    from graphembedding_amd.model_mse import SiameseGCNTNMSE
+    prob = small_problem(n_graphs=4, n_pairs=3, seed=3)
+    model = SiameseGCNTNMSE(prob.d_in, prob.flags, device='cpu', params=prob.params)
+    train = {model._seed(None) + k for k in range(-50, 50)}
+    for step in range(20):
+        model.step_count = step
+        assert model.val_seed() not in train
+        assert model.val_seed(123) == 123
