@@ -638,6 +638,9 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #pragma unroll
         for (int r = 0; r < 3; ++r) d2[0][r] = d2[1][r] = 0.f;
       } else {
+      // the K0 + K1 Dense row sums run step-interleaved (row_sum16_n): slot r of side 0,
+      // K0 + r of side 1
+      float zs[K0 + K1];
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         if (r < K0 || r < K1) {
@@ -648,18 +651,28 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
               const bool k2 = (s ? (h >> 16) : (h & 0xFFFFu)) < A.thr2;
               d2[s][r] = k2 ? h2[s][r] * A.ik2 : 0.f;
               kb |= (k2 ? 1u : 0u) << (3 * s + r);
-              const float z = row_sum16(d2[s][r] * wdv) + bd;
-              const bool k4 = (km4 >> (16 * s + 4 * r)) & 1u;   // includes n < Ns
-              xo[s][r] = ((z > 0.f) & k4) ? z * A.ik4 : 0.f;
+              zs[s * K0 + r] = d2[s][r] * wdv;
             } else {
               d2[s][r] = 0.f;
-              xo[s][r] = 0.f;
             }
           }
         } else {
-          d2[0][r] = d2[1][r] = xo[0][r] = xo[1][r] = 0.f;
+          d2[0][r] = d2[1][r] = 0.f;
         }
       }
+      row_sum16_n(zs);
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          if (r < (s ? K1 : K0)) {
+            const float z = zs[s * K0 + r] + bd;
+            const bool k4 = (km4 >> (16 * s + 4 * r)) & 1u;   // includes n < Ns
+            xo[s][r] = ((z > 0.f) & k4) ? z * A.ik4 : 0.f;
+          } else {
+            xo[s][r] = 0.f;
+          }
+        }
       // publish x1 | x2 for the lanes that need every element
       if (j < 3) {
         const float v0 = j == 0 ? xo[0][0] : (j == 1 ? xo[0][1] : xo[0][2]);
@@ -743,11 +756,12 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         float x1[DN];
 #pragma unroll
         for (int a = 0; a < BL0; ++a) x1[a] = sX[a];
+        // the RA + RB row sums run step-interleaved: slot r of side 0, RA + r of side 1
+        float tt[RA + RB];
 #pragma unroll
         for (int r = 0; r < RN; ++r) {
           const int a = 4 * r + g;
           const int ac = a < DN ? a : 0;
-          ge[0][r] = ge[1][r] = 0.f;
           if (r < RA) {
             if constexpr (!AVG) {
               const float c = gmk * xo[0][r];
@@ -755,8 +769,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
               for (int b = 0; b < BL1; ++b) gWn[r][b] = fmaf(c, x2[b], gWn[r][b]);
               gVa[r] = fmaf(gmk, xo[0][r], gVa[r]);
             }
-            const float t1 = gmk4 * (sV[kc * VS + ac] + u[r]);
-            ge[0][r] = row_sum16(t1);
+            tt[r] = gmk4 * (sV[kc * VS + ac] + u[r]);
           }
           if (r < RB) {
             if constexpr (!AVG) gVb[r] = fmaf(gmk, xo[1][r], gVb[r]);
@@ -764,9 +777,14 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
             float w = 0.f;
 #pragma unroll
             for (int aa = 0; aa < BL0; ++aa) w = fmaf(x1[aa], wb[aa], w);
-            const float t2 = gmk4 * (sV[kc * VS + DN + ac] + w);
-            ge[1][r] = row_sum16(t2);
+            tt[RA + r] = gmk4 * (sV[kc * VS + DN + ac] + w);
           }
+        }
+        row_sum16_n(tt);
+#pragma unroll
+        for (int r = 0; r < RN; ++r) {
+          ge[0][r] = r < RA ? tt[r] : 0.f;
+          ge[1][r] = r < RB ? tt[RA + r] : 0.f;
         }
       }
 
@@ -883,6 +901,8 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         const int KS = s ? K1 : K0;
         // one-hot Xᵀ for gW0 as a bf16 A operand: row i = j ↔ type 16τ + j, k-slot
         // 8g + e ↔ node row 4g + (e & 3) (both halves: parts h | m of gZ0)
+        // A side of at most 8 nodes has only rows 4g, 4g+1: the h, l and m parts of both
+        // fit one MFMA's 8 k-slots (A = (o | o | o | 0), B = (h | l | m | h)).
         uint4 ohA[2], ohL[2];
 #pragma unroll
         for (int tau = 0; tau < 2; ++tau) {
@@ -893,8 +913,12 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
             o[q] = (q < KS && tq == (uint32_t)(16 * tau + j)) ? 0x3F80u : 0u;   // bf16 1.0
           }
           const uint32_t o01 = o[0] | (o[1] << 16), o23 = o[2];
-          ohA[tau] = uint4{o01, o23, o01, o23};
-          ohL[tau] = uint4{o01, o23, 0u, 0u};
+          if (KS > 2) {
+            ohA[tau] = uint4{o01, o23, o01, o23};
+            ohL[tau] = uint4{o01, o23, 0u, 0u};
+          } else {
+            ohA[tau] = uint4{o01, o01, o01, 0u};
+          }
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -913,12 +937,18 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           // then the l parts (rows 4g+3 of gZ0 are always zero)
           uint32_t h01, m01, l01, h23 = 0u, m23 = 0u, l23 = 0u;
           split3(gz0[0], gz0[1], h01, m01, l01);
-          if (KS > 2) split3(gz0[2], 0.f, h23, m23, l23);
-          const uint4 bhm = {h01, h23, m01, m23}, bl = {l01, l23, 0u, 0u};
+          if (KS > 2) {
+            split3(gz0[2], 0.f, h23, m23, l23);
+            const uint4 bhm = {h01, h23, m01, m23}, bl = {l01, l23, 0u, 0u};
 #pragma unroll
-          for (int tau = 0; tau < 2; ++tau) {
-            gw0[tau][t] = mfbf(ohL[tau], bl, gw0[tau][t]);
-            gw0[tau][t] = mfbf(ohA[tau], bhm, gw0[tau][t]);
+            for (int tau = 0; tau < 2; ++tau) {
+              gw0[tau][t] = mfbf(ohL[tau], bl, gw0[tau][t]);
+              gw0[tau][t] = mfbf(ohA[tau], bhm, gw0[tau][t]);
+            }
+          } else {   // the fourth B dword meets a zero A dword: any finite value
+            const uint4 b = {h01, l01, m01, h01};
+#pragma unroll
+            for (int tau = 0; tau < 2; ++tau) gw0[tau][t] = mfbf(ohA[tau], b, gw0[tau][t]);
           }
         }
       }

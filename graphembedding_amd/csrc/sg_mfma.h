@@ -69,5 +69,20 @@ __device__ __forceinline__ float row_sum16(float v) {
   return v;
 }
 
+// row_sum16 of N independent values, step-interleaved: a DPP read of a VGPR written by
+// the previous VALU instruction needs two wait states (s_nop 1 in a lone chain); with
+// N >= 3 chains advanced in lockstep the other chains' adds fill them
+template <int N>
+__device__ __forceinline__ void row_sum16_n(float (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp<0xB1>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp<0x4E>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp<0x141>(v[i]);
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] += dpp<0x140>(v[i]);
+}
+
 
 }  // namespace sgk
