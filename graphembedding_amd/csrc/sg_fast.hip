@@ -274,7 +274,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
     stv[k] = i < nprm ? prm[i] : 0.f;
   }
 
-  float *sW0 = smem;                            // W0 · ik0, row d_in zero
+  float *sW0 = smem;                            // W0 · ik0 · ik1, row d_in zero
   float *sWa = sW0 + (d_in + 1) * FH1;          // [a][k][12]: W[a][b][k] at b
   float *sWb = sWa + DN * FK * WR;              // [b][k][WR]: W[a][b][k] at a
   float *sV = sWb + DN * FK * WR;               // [k][VS]
@@ -292,7 +292,8 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   // unused until the pair loop) in one pass with all loads in flight, and the
   // tables are built from there: one global-load latency instead of one per table.
   // Dropout scales are folded into the tables that feed the dropped tensors:
-  // Z0 = (W0 · ik0)[type] and gP1 = keep·relu' · (gZ1 (W1 · ik1)ᵀ).
+  // Z0 = (W0 · ik0 · ik1)[type] (with b0 · ik1: P1 comes out scaled by the layer-1
+  // dropout scale, relu(ik1 x) = ik1 relu(x)) and gP1 = keep·relu' · (gZ1 (W1 · ik1)ᵀ).
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int i = k * bdx + tid;
@@ -316,7 +317,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   }
   __syncthreads();
   for (int i = tid; i < (d_in + 1) * FH1; i += blockDim.x)
-    sW0[i] = i < d_in * FH1 ? stg[A.oW0 + i] * A.ik0 : 0.f;
+    sW0[i] = i < d_in * FH1 ? stg[A.oW0 + i] * (A.ik0 * A.ik1) : 0.f;
   for (int i = tid; i < DN * FK * WR; i += blockDim.x) {
     const int x = i / (FK * WR), rem = i - x * FK * WR, k = rem / WR, y = rem - k * WR;
     sWa[i] = y < DN ? stg[A.oW + (x * DN + y) * FK + k] : 0.f;
@@ -345,9 +346,11 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #endif
   // per-lane parameters, also from the staged copy
   const int j_ = tid & 15;
-  const float b0v0 = stg[A.ob0 + j_], b0v1 = stg[A.ob0 + 16 + j_];
+  const float b0v0 = stg[A.ob0 + j_] * A.ik1, b0v1 = stg[A.ob0 + 16 + j_] * A.ik1;
   const float b1v = stg[A.ob1 + j_];
-  const float wdv = AVG ? 0.f : stg[A.oWd + j_];
+  // Dense weight with the layer-2 dropout scale folded in (D2 is kept unscaled; the
+  // Dense weight gradient takes ik2 at the flush)
+  const float wdv = AVG ? 0.f : stg[A.oWd + j_] * A.ik2;
   const float bd = AVG ? 0.f : stg[A.obd];
   const bool kv = j_ < FK;
   const int kc = kv ? j_ : FK - 1;
@@ -542,7 +545,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         }
         tys[s] = tp;
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {   // P1 = Â Z0 + b0  (rows of absent nodes: b0, never read)
+        for (int t = 0; t < 2; ++t) {   // ik1 · P1 = Â Z0 + ik1 b0  (absent rows: ik1 b0, never read)
           const float bb = t ? b0v1 : b0v0;
           f4 acc = {bb, bb, bb, bb};
 #pragma unroll
@@ -550,7 +553,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           p1[s][t] = acc;
         }
       }
-      // H1 = relu(P1), D1 = dropout(H1): one hash per element (node 4r+g, feature
+      // D1 = dropout(ik1 relu(P1)): one hash per element (node 4r+g, feature
       // 16t+j) gives both sides' draws.  The backward reads keep·relu' back as D1 > 0.
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
@@ -563,7 +566,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
               float *T = sT + s * 16 * TS1 + (4 * g + r) * TS1 + 16 * t + j;
               if (r < (s ? K1 : K0)) {
                 const uint32_t d = s ? (h >> 16) : (h & 0xFFFFu);
-                const float v = fmaxf(p1[s][t][r] * A.ik1, 0.f);
+                const float v = fmaxf(p1[s][t][r], 0.f);
                 *T = d < A.thr1 ? v : 0.f;
               } else {
                 *T = 0.f;
@@ -649,7 +652,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           for (int s = 0; s < 2; ++s) {
             if (r < (s ? K1 : K0)) {
               const bool k2 = (s ? (h >> 16) : (h & 0xFFFFu)) < A.thr2;
-              d2[s][r] = k2 ? h2[s][r] * A.ik2 : 0.f;
+              d2[s][r] = k2 ? h2[s][r] : 0.f;   // D2 / ik2
               kb |= (k2 ? 1u : 0u) << (3 * s + r);
               zs[s * K0 + r] = d2[s][r] * wdv;
             } else {
@@ -820,7 +823,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
             const float gp = xo[s][r] > 0.f ? ge[s][r] : 0.f;   // dropout4 · relu' · present
             gwda = fmaf(d2[s][r], gp, gwda);
             gbda += gp;   // equal on the 16 lanes of a row: lane j == 0 is flushed
-            const float v = ((kb >> (3 * s + r)) & 1u) ? gp * wdv * A.ik2 : 0.f;
+            const float v = ((kb >> (3 * s + r)) & 1u) ? gp * wdv : 0.f;
             gb1a += v;
             gh2[s][r] = v;
           }
@@ -977,7 +980,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
     gb0a0 = xsum32(xsum16(gb0a0));
     gb0a1 = xsum32(xsum16(gb0a1));
     gb1a = xsum32(xsum16(gb1a));
-    gwda = xsum32(xsum16(gwda));
+    gwda = xsum32(xsum16(gwda)) * A.ik2;
     gbda = xsum32(xsum16(gbda));
   }
   float *F = smem;

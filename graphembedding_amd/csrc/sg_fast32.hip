@@ -152,7 +152,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
   const float *__restrict__ prm = A.params;
 
   // ---- parameter staging (behind the shared tables) and tables ----
-  float *sW0 = smem;                            // W0 · ik0, row d_in zero
+  float *sW0 = smem;                            // W0 · ik0 · ik1, row d_in zero
   float *sWa = sW0 + (d_in + 1) * FH1;          // [a][k][WAS]: W[a][b][k] at b
   float *sV = sWa + NC * FK * WAS;              // [k][VS]
   float *sW1 = sV + FK * VS;                    // W1 · ik1 [32][W1S]
@@ -176,7 +176,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
   }
   __syncthreads();
   for (int i = tid; i < (d_in + 1) * FH1; i += blockDim.x)
-    sW0[i] = i < d_in * FH1 ? stg[A.oW0 + i] * A.ik0 : 0.f;
+    sW0[i] = i < d_in * FH1 ? stg[A.oW0 + i] * (A.ik0 * A.ik1) : 0.f;
   for (int i = tid; i < NC * FK * WAS; i += blockDim.x) {
     const int row = i / WAS, b = i - row * WAS, a = row / FK, k = row - a * FK;
     sWa[row * WAS + 4 * ((b >> 2) ^ wa_swz(k, a)) + (b & 3)] =
@@ -191,9 +191,12 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
     sW1[(i / FH2) * W1S + i % FH2] = w * A.ik1;
     sW1T[(i % FH2) * W1TS + i / FH2] = w;
   }
-  const float b0v0 = stg[A.ob0 + j], b0v1 = stg[A.ob0 + 16 + j];
+  // P1 comes out scaled by ik1 (relu(ik1 x) = ik1 relu(x)): W0 and b0 carry it
+  const float b0v0 = stg[A.ob0 + j] * A.ik1, b0v1 = stg[A.ob0 + 16 + j] * A.ik1;
   const float b1v = stg[A.ob1 + j];
-  const float wdv = stg[A.oWd + j];
+  // Dense weight with the layer-2 dropout scale folded in (D2 kept unscaled; the Dense
+  // weight gradient takes ik2 at the flush)
+  const float wdv = stg[A.oWd + j] * A.ik2;
   const float bd = stg[A.obd];
   const bool kv = j < FK;
   const int kc = kv ? j : FK - 1;
@@ -383,7 +386,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
       }
     };
 
-    // ================= forward: P1 = Â Z0 + b0 =================
+    // ================= forward: ik1 · P1 = Â Z0 + ik1 b0 =================
     uint32_t tyA[2][2];     // [s][tile]: types of node rows 4g+r, 6 bits; 63 = dropped/absent
     f4 d1[2][2][2];         // [s][to][f]: P1, then D1 in place
 #pragma unroll
@@ -422,7 +425,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
       tyA[s][0] = tp[0];
       tyA[s][1] = tp[1];
     }
-    // D1 = dropout(relu(P1)): one hash per element (node 16to+4r+g, feature 16f+j)
+    // D1 = dropout(ik1 relu(P1)): one hash per element (node 16to+4r+g, feature 16f+j)
     // gives both sides' draws; k-blocks past a side's nodes are zeroed
 #pragma unroll
     for (int to = 0; to < 2; ++to)
@@ -437,7 +440,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
               const uint32_t dr = s ? (h >> 16) : (h & 0xFFFFu);
-              const float v = fmaxf(d1[s][to][f][r] * A.ik1, 0.f);
+              const float v = fmaxf(d1[s][to][f][r], 0.f);
               d1[s][to][f][r] = (nb < (s ? KB1 : KB0) && dr < A.thr1) ? v : 0.f;
             }
           } else {
@@ -501,7 +504,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
         for (int s = 0; s < 2; ++s) {
           if (nb < (s ? KB1 : KB0)) {
             const bool k2 = (s ? (h >> 16) : (h & 0xFFFFu)) < A.thr2;
-            d2[s][nb] = k2 ? h2[s][to][r] * A.ik2 : 0.f;
+            d2[s][nb] = k2 ? h2[s][to][r] : 0.f;   // D2 / ik2
             kb2[s] |= (k2 ? 1u : 0u) << nb;
             const float z = row_sum16(d2[s][nb] * wdv) + bd;
             const bool k4 = (km4[s] >> (16 * to + 4 * r + g)) & 1u;   // includes n < N
@@ -643,7 +646,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
             const float gp = xo[s][nb] > 0.f ? ge[s][nb] : 0.f;
             gwda = fmaf(d2[s][nb], gp, gwda);
             gbda += gp;
-            const float v = ((kb2[s] >> nb) & 1u) ? gp * wdv * A.ik2 : 0.f;
+            const float v = ((kb2[s] >> nb) & 1u) ? gp * wdv : 0.f;
             gb1a += v;
             gh2[to][r] = v;
           }
@@ -733,7 +736,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
   gb0a0 = xsum32(xsum16(gb0a0));
   gb0a1 = xsum32(xsum16(gb0a1));
   gb1a = xsum32(xsum16(gb1a));
-  gwda = xsum32(xsum16(gwda));
+  gwda = xsum32(xsum16(gwda)) * A.ik2;
   gbda = xsum32(xsum16(gbda));
   float *F = smem;
   __syncthreads();
