@@ -147,3 +147,29 @@ def test_c5_web_sampled_pairs(gpu):
     pairs = batch.pairs.cpu().numpy()[idx]
     ref = _oracle_scores(model, f, gs, pairs, idx, seed)
     np.testing.assert_allclose(s[idx], ref, rtol=TOL, atol=TOL)
+
+
+def test_c2_fused_scores_cover_every_pair(gpu):
+    """Every pair of a launch is scored exactly where it belongs: fused fwd_bwd's s_out
+    (NaN-filled before the launch) equals the forward-only scores bit for bit, class
+    order on and off, at an emulated 8-rank shard (61,250 pairs) and the full step."""
+    import torch
+    from graphembedding_amd.allpairs import AllPairsShard, load_graph_set
+    from graphembedding_amd.config import Flags
+    from graphembedding_amd.model_mse import SiameseGCNTNMSE
+    f = Flags(dropout=0.1)
+    gs = load_graph_set('syn_aids700nef', n_max=10)
+    labels = gs.label_matrix(f.yeta)
+    model = SiameseGCNTNMSE(gs.d_in, f, device=gpu, n_max=gs.n_max)
+    seed = 99
+    for world in (8, 1):
+        shard = AllPairsShard(gs, labels, 0, world, device=gpu)
+        for balance in (False, True):
+            batch = shard.batch(model, balance=balance)
+            if balance:
+                o = np.sort(batch.order.cpu().numpy())
+                assert np.array_equal(o, np.arange(batch.n_pairs)), 'order is not a permutation'
+            so = torch.full((batch.n_pairs,), float('nan'), dtype=torch.float32, device=gpu)
+            model.fwd_bwd(batch, seed=seed, s_out=so)
+            assert int(torch.isnan(so).sum()) == 0, (world, balance)
+            assert torch.equal(so, model.pred_sim_without_act(batch, seed=seed)), (world, balance)

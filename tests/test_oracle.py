@@ -9,7 +9,17 @@ import torch
 from _fixtures import AVERAGE_STACK, small_problem
 from oracle import siamese_oracle as O
 
-torch.set_default_dtype(torch.float64)
+
+
+@pytest.fixture(autouse=True, scope='module')
+def _float64_default():
+    """float64 for this module's torch restatement only: a module-level
+    set_default_dtype would leak into every test collected after it (the GPU tests'
+    float32 buffers included)."""
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    yield
+    torch.set_default_dtype(old)
 
 
 def _act(name, x):
