@@ -161,3 +161,37 @@ def test_fast_path_matches_generic_path(gpu, monkeypatch, stack):
     np.testing.assert_allclose(s_fast, s_gen, rtol=1e-5, atol=1e-5)
     _check_grad(g_fast, g_gen, tol=2e-5)
     assert abs(l_fast - float(model.loss_buf[0].item())) <= 1e-5 * max(1.0, abs(l_fast))
+
+
+@pytest.mark.parametrize('case', ['one_type', 'types_32', 'nmax12', 'heavy_dropout',
+                                  'self_and_repeated_pairs'])
+def test_fused_path_edge_shapes(gpu, case):
+    """Fused-kernel boundaries against the oracle: a single node type (d_in = 1), the
+    largest one-hot width the fused kernel takes (d_in = 32), Padding / NTN width 12 with
+    12-node graphs (the third Â k-step full), dropout 0.9 (most elements dropped), and
+    self-pairs (g, g) plus repeated pairs (distinct pair keys, so distinct masks)."""
+    kw = dict(n_graphs=14, n_pairs=48, seed=17)
+    if case == 'one_type':
+        kw.update(n_types=1)
+    elif case == 'types_32':
+        kw.update(n_types=32, n_lo=8, n_hi=10, n_graphs=40)
+    elif case == 'nmax12':
+        kw.update(n_max=12, n_lo=9, n_hi=12)
+    elif case == 'heavy_dropout':
+        kw.update(flags_overrides=dict(dropout=0.9))
+    prob = small_problem(**kw)
+    if case == 'self_and_repeated_pairs':
+        prob.pairs[:16, 1] = prob.pairs[:16, 0]
+        prob.pairs[16:24] = prob.pairs[0]
+    if case == 'types_32':
+        assert prob.d_in > 16, prob.d_in   # the second 16-type tile of the gW0 product
+    model, batch = prob.make_gpu_model(device=gpu)
+    assert model.kernel_path == 1, (case, model.kernel_path)
+    seed = 4321
+    s = model.pred_sim_without_act(batch, seed=seed).cpu().numpy()
+    ref = run_oracle_step(prob, seed)
+    np.testing.assert_allclose(s, ref.s, rtol=TOL, atol=TOL)
+    model.fwd_bwd(batch, seed=seed)
+    _check_grad(model.grad.cpu().numpy(), ref.grad_mse)
+    loss_mse = float(model.loss_buf[0].item())
+    assert abs(loss_mse - ref.loss_mse) <= TOL * max(1.0, abs(ref.loss_mse))
