@@ -49,7 +49,12 @@ def build_hip(force: bool = False, verbose: bool = False, out: str = None, defin
         procs, objs = [], []
         for src in SOURCES:
             obj = os.path.join(tmp, src + '.o')
-            cmd = base + SOURCE_FLAGS.get(src, []) + ['-c', os.path.join(CSRC, src), '-o', obj]
+            # A/B of one source's options: SG_FLAGS_SG_FAST="..." replaces sg_fast.hip's
+            flags = SOURCE_FLAGS.get(src, [])
+            env_key = 'SG_FLAGS_' + src.split('.')[0].upper()
+            if env_key in os.environ:
+                flags = os.environ[env_key].split()
+            cmd = base + flags + ['-c', os.path.join(CSRC, src), '-o', obj]
             if verbose:
                 print(' '.join(cmd))
             procs.append((src, subprocess.Popen(cmd, cwd=CSRC, stdout=subprocess.PIPE,

@@ -46,6 +46,25 @@ constexpr int W1TS = 36; // W1ᵀ table row stride (32 + pad)
 #ifndef SG_GD1_BF16
 #define SG_GD1_BF16 1
 #endif
+// Scheduling fences around each f32 MFMA product (SG_MFMA_CLUSTER = 1: all but gZ0,
+// 2: all): its MFMAs then issue back to back instead of one at a time between VALU
+// instructions.  On gfx950 every switch between v_mfma_f32_16x16x4_f32 and VALU in a
+// wave's stream costs issue cycles (scripts/mfma_valu_mix.hip: 4 MFMAs + 48 FMAs take
+// 16% longer interleaved than grouped); the scheduler's default is to interleave.
+// Measured 470.3 -> 480.7 M pairs/s (level 2); fencing the bf16 gD1 MFMAs too: 477.3.
+#ifndef SG_MFMA_CLUSTER
+#define SG_MFMA_CLUSTER 2
+#endif
+#if SG_MFMA_CLUSTER
+#define SG_CLUSTER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define SG_CLUSTER() do {} while (0)
+#endif
+#if SG_MFMA_CLUSTER >= 2
+#define SG_CLUSTER2() __builtin_amdgcn_sched_barrier(0)
+#else
+#define SG_CLUSTER2() do {} while (0)
+#endif
 #ifndef SG_FAST_MAXW
 #define SG_FAST_MAXW 8
 #endif
@@ -544,6 +563,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           }
         }
         tys[s] = tp;
+        SG_CLUSTER();
 #pragma unroll
         for (int t = 0; t < 2; ++t) {   // ik1 · P1 = Â Z0 + ik1 b0  (absent rows: ik1 b0, never read)
           const float bb = t ? b0v1 : b0v0;
@@ -552,6 +572,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           for (int q = 0; q < KS; ++q) acc = mfma4(af[s][q], z0[t][q], acc);
           p1[s][t] = acc;
         }
+        SG_CLUSTER();
       }
       // D1 = dropout(ik1 relu(P1)): one hash per element (node 4r+g, feature
       // 16t+j) gives both sides' draws.  The backward reads keep·relu' back as D1 > 0.
@@ -585,6 +606,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         const f4 lo = *(const f4 *)sTp, hi = *(const f4 *)(sTp + 4);
         const f4 wlo = *(const f4 *)w1bp, whi = *(const f4 *)(w1bp + 4);
         f4 z1 = {0.f, 0.f, 0.f, 0.f};
+        SG_CLUSTER();
 #pragma unroll
         for (int q = 0; q < 4; ++q) z1 = mfma4(lo[q], wlo[q], z1);
 #pragma unroll
@@ -596,6 +618,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           acc = mfma4(af[s][1], z1[2 * s + 1], acc);
           h2[s] = acc;
         }
+        SG_CLUSTER();
       } else {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {   // Z1 = D1 W1 ; H2 = Â Z1 + b1
@@ -604,6 +627,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           const f4 lo = *(const f4 *)T, hi = *(const f4 *)(T + 4);
           const f4 wlo = *(const f4 *)w1bp, whi = *(const f4 *)(w1bp + 4);
           f4 z1 = {0.f, 0.f, 0.f, 0.f};
+          SG_CLUSTER();
 #pragma unroll
           for (int q = 0; q < 4; ++q) z1 = mfma4(lo[q], wlo[q], z1);
 #pragma unroll
@@ -612,6 +636,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #pragma unroll
           for (int q = 0; q < KS; ++q) acc = mfma4(af[s][q], z1[q], acc);
           h2[s] = acc;
+          SG_CLUSTER();
         }
       }
       // D2 = dropout(H2) (one hash per element, both sides); zpre = D2·Wd + bd;
@@ -832,11 +857,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         //   gz1  rows = nodes (B of gW1 = D1ᵀ gZ1),  gz1t rows = j (A of gD1 = gZ1 W1ᵀ)
         f4 gz1 = {0.f, 0.f, 0.f, 0.f};
         gz1t[s] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < KS; ++q) {
-          gz1 = mfma4(af[s][q], gh2[s][q], gz1);
-          if (!PACK) gz1t[s] = mfma4(gh2[s][q], af[s][q], gz1t[s]);
-        }
         // this lane's D1 entries: A operand of gW1 += D1ᵀ gZ1 and, as D1 > 0, the
         // keep·relu' mask of gP1
         const float *T1 = sT + s * 16 * TS1 + 4 * g * TS1 + j;
@@ -844,20 +864,30 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int q = 0; q < KS; ++q) dq[s][t][q] = T1[q * TS1 + 16 * t];
+        SG_CLUSTER();
+#pragma unroll
+        for (int q = 0; q < KS; ++q) {
+          gz1 = mfma4(af[s][q], gh2[s][q], gz1);
+          if (!PACK) gz1t[s] = mfma4(gh2[s][q], af[s][q], gz1t[s]);
+        }
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int q = 0; q < KS; ++q) gw1[t] = mfma4(dq[s][t][q], gz1[q], gw1[t]);
+        SG_CLUSTER();
       }
       if constexpr (PACK) {
         // gZ1ᵀ of both sides in the shared layout: side 0's Â rows are zero on the
         // lanes of side 1's rows (nodes >= 8 are absent), afp holds side 1's rows there
         f4 c = {0.f, 0.f, 0.f, 0.f};
+        const float afp0 = W[afp[0]], afp1 = W[afp[1]];
+        SG_CLUSTER();
         c = mfma4(gh2[0][0], af[0][0], c);
         c = mfma4(gh2[0][1], af[0][1], c);
-        c = mfma4(gh2[1][0], W[afp[0]], c);
-        c = mfma4(gh2[1][1], W[afp[1]], c);
+        c = mfma4(gh2[1][0], afp0, c);
+        c = mfma4(gh2[1][1], afp1, c);
         gz1t[0] = c;
+        SG_CLUSTER();
       }
       // gD1 · ik1 = gZ1 (W1 ik1)ᵀ per feature tile t (one chain per tile when packed)
       f4 gd[2][2];   // [side, or 0 = shared][t]
@@ -934,8 +964,10 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           if (t) gb0a1 += (gp1[0] + gp1[1]) + gp1[2];
           else gb0a0 += (gp1[0] + gp1[1]) + gp1[2];
           f4 gz0 = {0.f, 0.f, 0.f, 0.f};  // gZ0 = Âᵀ gP1
+          SG_CLUSTER2();
 #pragma unroll
           for (int q = 0; q < KS; ++q) gz0 = mfma4(af[s][q], gp1[q], gz0);
+          SG_CLUSTER2();
           // gW0 / ik0 += Xᵀ gZ0: B k-slots 8g + e = (h | m) parts of node rows 4g + e,
           // then the l parts (rows 4g+3 of gZ0 are always zero)
           uint32_t h01, m01, l01, h23 = 0u, m23 = 0u, l23 = 0u;
