@@ -50,7 +50,7 @@ constexpr int W1TS = 36; // W1ᵀ table row stride (32 + pad)
 // 2: all): its MFMAs then issue back to back instead of one at a time between VALU
 // instructions.  On gfx950 every switch between v_mfma_f32_16x16x4_f32 and VALU in a
 // wave's stream costs issue cycles (scripts/mfma_valu_mix.hip: 4 MFMAs + 48 FMAs take
-// 16% longer interleaved than grouped); the scheduler's default is to interleave.
+// 7.6% longer interleaved than grouped); the scheduler's default is to interleave.
 // Measured 470.3 -> 480.7 M pairs/s (level 2); fencing the bf16 gD1 MFMAs too: 477.3.
 #ifndef SG_MFMA_CLUSTER
 #define SG_MFMA_CLUSTER 2

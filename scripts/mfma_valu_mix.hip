@@ -5,7 +5,8 @@
 //   mode 3: grouped, the 4 MFMAs back to back then the 48 fma
 //           (sched_group_barrier pins the order);
 // for v_mfma_f32_16x16x4_f32 and v_mfma_f32_16x16x32_bf16, 1 and 2 waves per SIMD.
-// Cycles per iteration per wave from s_memtime.
+// Cycles per iteration per wave from s_memtime.  Build with -fno-slp-vectorize (as the
+// library): otherwise the FMAs are packed into v_pk_fma_f32.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 typedef float f4 __attribute__((ext_vector_type(4)));

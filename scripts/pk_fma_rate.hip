@@ -1,7 +1,8 @@
 // Microbenchmark: issue cost of packed FP32 (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32,
 // two floats per lane) against v_fma_f32, alone and between f32 MFMAs.  Each wave runs
 // ITER iterations over 24 independent chains; cycles per instruction per wave from
-// s_memtime, one block per CU at 1 and 2 waves per SIMD.
+// s_memtime, one block per CU at 1 and 2 waves per SIMD.  Build with -fno-slp-vectorize,
+// or the scalar FMA case is packed as well.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 typedef float f2 __attribute__((ext_vector_type(2)));
