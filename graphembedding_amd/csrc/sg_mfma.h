@@ -16,8 +16,8 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
 // ---- split-bf16 gW0 product ---------------------------------------------------
 // v_mfma_f32_16x16x4_f32 runs on the vector FP32 datapath (it never overlaps VALU
 // on gfx950, scripts/mfma_coexec.hip).  The one-hot operand of gW0 = Xᵀ·gZ0 is
-// exact in bf16, so gZ0 is carried as x = h + m + l (three RNE bf16 parts, each
-// residual exact in f32, |l| <= 2^-16 |x|) and the product runs on
+// exact in bf16, so gZ0 is carried as x = h + m + l (three bf16 parts, each residual
+// exact in f32, split3 below) and the product runs on
 // v_mfma_f32_16x16x32_bf16: 1.0 × part is exact, accumulation is f32.
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf2v __attribute__((ext_vector_type(2)));
@@ -26,13 +26,36 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {   // v_cvt_pk_bf
   const bf2v v = {(__bf16)a, (__bf16)b};
   return __builtin_bit_cast(uint32_t, v);
 }
-// (x0, x1) -> packed bf16 pairs of the h, m, l parts (x = h + m + l)
+// (x0, x1) -> packed bf16 pairs of the h, m, l parts (x = h + m + l + e)
+#ifndef SG_SPLIT_TRUNC
+#define SG_SPLIT_TRUNC 1
+#endif
+#if SG_SPLIT_TRUNC
+// Truncating parts: h = x with the low 16 mantissa bits cleared (one AND), r = x - h and
+// r - m exact in f32, and the bf16 pairs are the high halves of (x0, x1) and of the
+// residuals, packed by v_perm_b32.  |e| < 2^-21 |x| (RNE parts: 2^-24), at 4 ANDs, 4 subs
+// and 3 perms per pair of values instead of 3 v_cvt_pk_bf16_f32 (twice the issue cost of
+// a plain VALU op on gfx950, scripts/valu_rates.hip), 4 unpacks and 4 subs.
+__device__ __forceinline__ uint32_t hi16x2(uint32_t a, uint32_t b) {   // hi16(a) | hi16(b) << 16
+  return __builtin_amdgcn_perm(b, a, 0x07060302u);
+}
+__device__ __forceinline__ void split3(float x0, float x1, uint32_t &h, uint32_t &m, uint32_t &l) {
+  const uint32_t u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);
+  h = hi16x2(u0, u1);
+  const float r0 = x0 - __uint_as_float(u0 & 0xFFFF0000u), r1 = x1 - __uint_as_float(u1 & 0xFFFF0000u);
+  const uint32_t v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
+  m = hi16x2(v0, v1);
+  const float s0 = r0 - __uint_as_float(v0 & 0xFFFF0000u), s1 = r1 - __uint_as_float(v1 & 0xFFFF0000u);
+  l = hi16x2(__float_as_uint(s0), __float_as_uint(s1));
+}
+#else
 __device__ __forceinline__ void split3(float x0, float x1, uint32_t &h, uint32_t &m, uint32_t &l) {
   h = pk_bf16(x0, x1);
   const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xFFFF0000u);
   m = pk_bf16(r0, r1);
   l = pk_bf16(r0 - __uint_as_float(m << 16), r1 - __uint_as_float(m & 0xFFFF0000u));
 }
+#endif
 __device__ __forceinline__ f4 mfbf(uint4 a, uint4 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a),
                                                   __builtin_bit_cast(bf8, b), c, 0, 0, 0);
