@@ -424,12 +424,15 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
                   {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}}};
   float gb0a0 = 0.f, gb0a1 = 0.f, gb1a = 0.f, gwda = 0.f, gbda = 0.f;
   constexpr int RW_ = AVG ? 1 : RN, DW_ = AVG ? 1 : DN;   // AVG: per-pair buffer instead
-  float gWn[RW_][DW_], gVa[RW_], gVb[RW_];
+  // the NTN head's FMAs run as v_pk_fma_f32 over element pairs (b, b + 1): one issue
+  // for two FMAs (scripts/pk_fma_rate.hip); the x / W rows are 8-byte aligned in LDS
+  f2 gWn[RW_][(DW_ + 1) / 2];
+  float gVa[RW_], gVb[RW_];
 #pragma unroll
   for (int r = 0; r < RW_; ++r) {
     gVa[r] = gVb[r] = 0.f;
 #pragma unroll
-    for (int b = 0; b < DW_; ++b) gWn[r][b] = 0.f;
+    for (int b = 0; b < (DW_ + 1) / 2; ++b) gWn[r][b] = f2{0.f, 0.f};
   }
   float gbn = 0.f, gUa = 0.f, lossa = 0.f;
   const float ybar = (BWD && !ALIGNED) ? A.y_stats[0] : 0.f;
@@ -721,9 +724,10 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       constexpr int BL0 = AVG ? DN : (4 * K0 < D ? 4 * K0 : D);
       constexpr int BL1 = AVG ? DN : (4 * K1 < D ? 4 * K1 : D);
       constexpr int RA = AVG ? RN : K0, RB = AVG ? RN : K1;   // row groups holding x_s
-      float x2[DN];
+      constexpr int BP0 = (BL0 + 1) / 2, BP1 = (BL1 + 1) / 2;   // element pairs
+      f2 x2[(DN + 1) / 2];
 #pragma unroll
-      for (int b = 0; b < BL1; ++b) x2[b] = sX[XO2 + b];
+      for (int b = 0; b < BP1; ++b) x2[b] = *(const f2 *)(sX + XO2 + 2 * b);
       float u[RN];
       float mpart = 0.f;
 #pragma unroll
@@ -732,9 +736,11 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         const int ac = a < DN ? a : 0;
         if (r < RA) {
           const float *wa = sWa + (ac * FK + kc) * WR;
-          float acc = 0.f;
+          f2 acc2 = {0.f, 0.f};
 #pragma unroll
-          for (int b = 0; b < BL1; ++b) acc = fmaf(wa[b], x2[b], acc);
+          for (int b = 0; b < BP1; ++b)
+            acc2 = __builtin_elementwise_fma(*(const f2 *)(wa + 2 * b), x2[b], acc2);
+          const float acc = acc2.x + acc2.y;
           u[r] = acc;
           // x1[a] u[a][k] + V[k][a] x1[a] + V[k][D+a] x2[a]   (x of invalid a is 0)
           mpart = fmaf(xo[0][r], acc + sV[kc * VS + ac], mpart);
@@ -781,9 +787,9 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       const float gmk4 = gmk * A.ik4;
       float ge[2][RN];   // dL/dx · ik4 (before the x > 0 mask)
       {
-        float x1[DN];
+        f2 x1[(DN + 1) / 2];
 #pragma unroll
-        for (int a = 0; a < BL0; ++a) x1[a] = sX[a];
+        for (int a = 0; a < BP0; ++a) x1[a] = *(const f2 *)(sX + 2 * a);
         // the RA + RB row sums run step-interleaved: slot r of side 0, RA + r of side 1
         float tt[RA + RB];
 #pragma unroll
@@ -793,8 +799,9 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           if (r < RA) {
             if constexpr (!AVG) {
               const float c = gmk * xo[0][r];
+              const f2 c2 = {c, c};
 #pragma unroll
-              for (int b = 0; b < BL1; ++b) gWn[r][b] = fmaf(c, x2[b], gWn[r][b]);
+              for (int b = 0; b < BP1; ++b) gWn[r][b] = __builtin_elementwise_fma(c2, x2[b], gWn[r][b]);
               gVa[r] = fmaf(gmk, xo[0][r], gVa[r]);
             }
             tt[r] = gmk4 * (sV[kc * VS + ac] + u[r]);
@@ -802,9 +809,11 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           if (r < RB) {
             if constexpr (!AVG) gVb[r] = fmaf(gmk, xo[1][r], gVb[r]);
             const float *wb = sWb + (ac * FK + kc) * WR;
-            float w = 0.f;
+            f2 w2 = {0.f, 0.f};
 #pragma unroll
-            for (int aa = 0; aa < BL0; ++aa) w = fmaf(x1[aa], wb[aa], w);
+            for (int aa = 0; aa < BP0; ++aa)
+              w2 = __builtin_elementwise_fma(x1[aa], *(const f2 *)(wb + 2 * aa), w2);
+            const float w = w2.x + w2.y;
             tt[RA + r] = gmk4 * (sV[kc * VS + DN + ac] + w);
           }
         }
@@ -932,11 +941,13 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int KS = s ? K1 : K0;
-        // one-hot Xᵀ for gW0 as a bf16 A operand: row i = j ↔ type 16τ + j, k-slot
-        // 8g + e ↔ node row 4g + (e & 3) (both halves: parts h | m of gZ0)
+        // one-hot Xᵀ for gW0 as a bf16 A operand: row i = j ↔ type 16τ + j.
+        // Three node rows per group (4g + q): three 16x16x16 MFMAs, k-slot 4g + e ↔ node
+        // row 4g + e, A = (o01 | o23) against the h, m and l parts of gZ0 in turn.
         // A side of at most 8 nodes has only rows 4g, 4g+1: the h, l and m parts of both
-        // fit one MFMA's 8 k-slots (A = (o | o | o | 0), B = (h | l | m | h)).
-        uint4 ohA[2], ohL[2];
+        // fit one 16x16x32 MFMA's 8 k-slots (A = (o | o | o | 0), B = (h | l | m | h)).
+        uint4 ohA[2];
+        uint2 oh2[2];
 #pragma unroll
         for (int tau = 0; tau < 2; ++tau) {
           uint32_t o[3];
@@ -947,8 +958,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           }
           const uint32_t o01 = o[0] | (o[1] << 16), o23 = o[2];
           if (KS > 2) {
-            ohA[tau] = uint4{o01, o23, o01, o23};
-            ohL[tau] = uint4{o01, o23, 0u, 0u};
+            oh2[tau] = uint2{o01, o23};
           } else {
             ohA[tau] = uint4{o01, o01, o01, 0u};
           }
@@ -968,17 +978,17 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #pragma unroll
           for (int q = 0; q < KS; ++q) gz0 = mfma4(af[s][q], gp1[q], gz0);
           SG_CLUSTER2();
-          // gW0 / ik0 += Xᵀ gZ0: B k-slots 8g + e = (h | m) parts of node rows 4g + e,
-          // then the l parts (rows 4g+3 of gZ0 are always zero)
+          // gW0 / ik0 += Xᵀ gZ0 (rows 4g+3 of gZ0 are always zero)
           uint32_t h01, m01, l01, h23 = 0u, m23 = 0u, l23 = 0u;
           split3(gz0[0], gz0[1], h01, m01, l01);
           if (KS > 2) {
             split3(gz0[2], 0.f, h23, m23, l23);
-            const uint4 bhm = {h01, h23, m01, m23}, bl = {l01, l23, 0u, 0u};
+            const uint2 bh = {h01, h23}, bm = {m01, m23}, bl = {l01, l23};
 #pragma unroll
             for (int tau = 0; tau < 2; ++tau) {
-              gw0[tau][t] = mfbf(ohL[tau], bl, gw0[tau][t]);
-              gw0[tau][t] = mfbf(ohA[tau], bhm, gw0[tau][t]);
+              gw0[tau][t] = mfbf16(oh2[tau], bl, gw0[tau][t]);
+              gw0[tau][t] = mfbf16(oh2[tau], bm, gw0[tau][t]);
+              gw0[tau][t] = mfbf16(oh2[tau], bh, gw0[tau][t]);
             }
           } else {   // the fourth B dword meets a zero A dword: any finite value
             const uint4 b = {h01, l01, m01, h01};
@@ -1034,7 +1044,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #pragma unroll
       for (int r = 0; r < RN; ++r)
 #pragma unroll
-        for (int b = 0; b < DN; ++b) Fw[64 * s++] = gWn[r][b];
+        for (int b = 0; b < DN; ++b) Fw[64 * s++] = gWn[r][b >> 1][b & 1];
 #pragma unroll
       for (int r = 0; r < RN; ++r) Fw[64 * s++] = gVa[r];
 #pragma unroll

@@ -8,6 +8,7 @@
 namespace sgk {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -39,13 +40,26 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {   // v_cvt_pk_bf
 __device__ __forceinline__ uint32_t hi16x2(uint32_t a, uint32_t b) {   // hi16(a) | hi16(b) << 16
   return __builtin_amdgcn_perm(b, a, 0x07060302u);
 }
+#ifndef SG_SPLIT_PK
+#define SG_SPLIT_PK 1
+#endif
 __device__ __forceinline__ void split3(float x0, float x1, uint32_t &h, uint32_t &m, uint32_t &l) {
   const uint32_t u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);
   h = hi16x2(u0, u1);
+#if SG_SPLIT_PK   // the two residual subtractions of each level as one v_pk_add_f32
+  const f2 r = f2{x0, x1} - f2{__uint_as_float(u0 & 0xFFFF0000u), __uint_as_float(u1 & 0xFFFF0000u)};
+  const float r0 = r.x, r1 = r.y;
+#else
   const float r0 = x0 - __uint_as_float(u0 & 0xFFFF0000u), r1 = x1 - __uint_as_float(u1 & 0xFFFF0000u);
+#endif
   const uint32_t v0 = __float_as_uint(r0), v1 = __float_as_uint(r1);
   m = hi16x2(v0, v1);
+#if SG_SPLIT_PK
+  const f2 t = f2{r0, r1} - f2{__uint_as_float(v0 & 0xFFFF0000u), __uint_as_float(v1 & 0xFFFF0000u)};
+  const float s0 = t.x, s1 = t.y;
+#else
   const float s0 = r0 - __uint_as_float(v0 & 0xFFFF0000u), s1 = r1 - __uint_as_float(v1 & 0xFFFF0000u);
+#endif
   l = hi16x2(__float_as_uint(s0), __float_as_uint(s1));
 }
 #else
@@ -59,6 +73,13 @@ __device__ __forceinline__ void split3(float x0, float x1, uint32_t &h, uint32_t
 __device__ __forceinline__ f4 mfbf(uint4 a, uint4 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a),
                                                   __builtin_bit_cast(bf8, b), c, 0, 0, 0);
+}
+// v_mfma_f32_16x16x16_bf16: 4 k-slots per lane (k = 4 (lane / 16) + e), two dwords per
+// operand, so a part that pairs with several others needs no duplicate registers
+typedef short s4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f4 mfbf16(uint2 a, uint2 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s4, a),
+                                                    __builtin_bit_cast(s4, b), c, 0, 0, 0);
 }
 
 // DPP lane move with bound_ctrl (no "old" operand to materialise), so the
