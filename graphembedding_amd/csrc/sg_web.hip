@@ -770,6 +770,101 @@ __global__ void __launch_bounds__(256) web_t_kernel(const float *__restrict__ X2
     }
 }
 
+// ---- the same T on bf16 MFMAs (SG_WEB_T_BF3, default): both operands are split on the
+// fly into three bf16 parts (x = h + m + l, sgk::split3: |x - h - m - l| < 2^-21 |x|)
+// and T accumulates hh + hm + mh + hl + lh + mm in f32 on v_mfma_f32_16x16x32_bf16:
+// 6 MFMAs of 16 cycles per 32-deep product instead of 8 f32 MFMAs of 32 cycles.
+// LDS: [part][128 rows][40 bf16] per operand (80-byte rows: the b128 fragment reads
+// of 8 consecutive rows fall on distinct banks), 60 KiB; 32-deep contraction chunks,
+// the next chunk's f32 operands prefetched into registers during the MFMAs.
+#ifndef SG_WEB_T_BF3
+#define SG_WEB_T_BF3 1
+#endif
+constexpr int B3K = 32, B3S = 40;   // contraction chunk, LDS row stride (bf16)
+constexpr int B3PART = TB * B3S;    // bf16 per part plane
+
+__device__ __forceinline__ void b3_split_store(uint16_t *plane, int r, int c, float4 x) {
+  uint32_t h01, m01, l01, h23, m23, l23;
+  sgk::split3(x.x, x.y, h01, m01, l01);
+  sgk::split3(x.z, x.w, h23, m23, l23);
+  const int o = r * B3S + c;
+  *(uint2 *)(plane + o) = uint2{h01, h23};
+  *(uint2 *)(plane + B3PART + o) = uint2{m01, m23};
+  *(uint2 *)(plane + 2 * B3PART + o) = uint2{l01, l23};
+}
+
+__global__ void __launch_bounds__(256) web_t_kernel_b3(const float *__restrict__ X2,
+                                                       const float *__restrict__ Wg,
+                                                       const int2 *__restrict__ ext128, int64_t n,
+                                                       int Dp, int K, float *__restrict__ Tout) {
+  __shared__ __attribute__((aligned(16))) uint16_t sA[3 * B3PART], sB[3 * B3PART];
+  const int64_t p0 = (int64_t)blockIdx.x * TB;
+  const int a0 = blockIdx.y * TB, k = blockIdx.z;
+  const int2 e = ext128[blockIdx.x];
+  if (a0 >= e.x) return;
+  const int nb = (e.y + B3K - 1) / B3K * B3K;   // x2 is zero past n2 (Dp is a multiple of 128)
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, i = l & 15, g = l >> 4;
+  const int wm = w >> 1, wn = w & 1;
+  const float *pa = X2 + p0 * Dp;
+  const float *pb = Wg + ((size_t)k * Dp + a0) * Dp;
+  float4 ra[4], rb[4];
+  auto load = [&](int b0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = tid + 256 * u, r = q >> 3, c = (q & 7) * 4;
+      ra[u] = *(const float4 *)(pa + (size_t)r * Dp + b0 + c);
+      rb[u] = *(const float4 *)(pb + (size_t)r * Dp + b0 + c);
+    }
+  };
+  f4 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f4{0.f, 0.f, 0.f, 0.f};
+  if (nb > 0) load(0);
+  for (int b0 = 0; b0 < nb; b0 += B3K) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = tid + 256 * u, r = q >> 3, c = (q & 7) * 4;
+      b3_split_store(sA, r, c, ra[u]);
+      b3_split_store(sB, r, c, rb[u]);
+    }
+    __syncthreads();
+    if (b0 + B3K < nb) load(b0 + B3K);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int oa = (wm * 64 + mi * 16 + i) * B3S + 8 * g;
+      const uint4 ah = *(const uint4 *)(sA + oa), am = *(const uint4 *)(sA + B3PART + oa),
+                  al = *(const uint4 *)(sA + 2 * B3PART + oa);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int ob = (wn * 64 + ni * 16 + i) * B3S + 8 * g;
+        const uint4 bh = *(const uint4 *)(sB + ob), bm = *(const uint4 *)(sB + B3PART + ob),
+                    bl = *(const uint4 *)(sB + 2 * B3PART + ob);
+        f4 c = acc[mi][ni];
+        c = sgk::mfbf(al, bh, c);
+        c = sgk::mfbf(ah, bl, c);
+        c = sgk::mfbf(am, bm, c);
+        c = sgk::mfbf(am, bh, c);
+        c = sgk::mfbf(ah, bm, c);
+        c = sgk::mfbf(ah, bh, c);
+        acc[mi][ni] = c;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t p = p0 + wm * 64 + mi * 16 + 4 * g + r;
+      if (p >= n) continue;
+      float *dst = Tout + ((size_t)p * K + k) * Dp + a0 + wn * 64 + i;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) dst[ni * 16] = acc[mi][ni][r];
+    }
+}
+
 // ---- gX2[p][b] += Σ_{k,a} gm[p][k] x1[p][a] W[a][b][k]  (grid: p-blocks × b-tiles) ----
 __global__ void __launch_bounds__(256) web_gx2_kernel(const float *__restrict__ X1,
                                                       const float *__restrict__ GM,
@@ -823,6 +918,85 @@ __global__ void __launch_bounds__(256) web_gx2_kernel(const float *__restrict__ 
       float *dst = GX2 + p * Dp + b0 + wn * 64 + i;
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) dst[ni * 16] += T.c[mi][ni][r];
+    }
+}
+
+// ---- gX2 on bf16 MFMAs (as web_t_kernel_b3): A = gm[p][k] x1[p][a] scaled while
+// staging, B = Wh[k][b][a]; 32-deep chunks of a for each k ----
+__global__ void __launch_bounds__(256) web_gx2_kernel_b3(const float *__restrict__ X1,
+                                                         const float *__restrict__ GM,
+                                                         const float *__restrict__ Wh,
+                                                         const int2 *__restrict__ ext128,
+                                                         int64_t n, int Dp, int K,
+                                                         float *__restrict__ GX2) {
+  __shared__ __attribute__((aligned(16))) uint16_t sA[3 * B3PART], sB[3 * B3PART];
+  const int64_t p0 = (int64_t)blockIdx.x * TB;
+  const int b0 = blockIdx.y * TB;
+  const int2 e = ext128[blockIdx.x];
+  if (b0 >= e.y) return;
+  const int na = (e.x + B3K - 1) / B3K * B3K;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, i = l & 15, g = l >> 4;
+  const int wm = w >> 1, wn = w & 1;
+  float4 ra[4], rb[4];
+  float gmr[4];
+  auto load = [&](int k, int a0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = tid + 256 * u, r = q >> 3, c = (q & 7) * 4;
+      const int64_t p = p0 + r;
+      gmr[u] = p < n ? GM[p * WKP + k] : 0.f;
+      ra[u] = *(const float4 *)(X1 + p * Dp + a0 + c);
+      rb[u] = *(const float4 *)(Wh + ((size_t)k * Dp + b0 + r) * Dp + a0 + c);
+    }
+  };
+  f4 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f4{0.f, 0.f, 0.f, 0.f};
+  const int steps = na / B3K, total = K * steps;
+  if (total > 0) load(0, 0);
+  for (int st = 0; st < total; ++st) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = tid + 256 * u, r = q >> 3, c = (q & 7) * 4;
+      const float gm = gmr[u];
+      b3_split_store(sA, r, c, make_float4(gm * ra[u].x, gm * ra[u].y, gm * ra[u].z, gm * ra[u].w));
+      b3_split_store(sB, r, c, rb[u]);
+    }
+    __syncthreads();
+    if (st + 1 < total) load((st + 1) / steps, ((st + 1) % steps) * B3K);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int oa = (wm * 64 + mi * 16 + i) * B3S + 8 * g;
+      const uint4 ah = *(const uint4 *)(sA + oa), am = *(const uint4 *)(sA + B3PART + oa),
+                  al = *(const uint4 *)(sA + 2 * B3PART + oa);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int ob = (wn * 64 + ni * 16 + i) * B3S + 8 * g;
+        const uint4 bh = *(const uint4 *)(sB + ob), bm = *(const uint4 *)(sB + B3PART + ob),
+                    bl = *(const uint4 *)(sB + 2 * B3PART + ob);
+        f4 c = acc[mi][ni];
+        c = sgk::mfbf(al, bh, c);
+        c = sgk::mfbf(ah, bl, c);
+        c = sgk::mfbf(am, bm, c);
+        c = sgk::mfbf(am, bh, c);
+        c = sgk::mfbf(ah, bm, c);
+        c = sgk::mfbf(ah, bh, c);
+        acc[mi][ni] = c;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t p = p0 + wm * 64 + mi * 16 + 4 * g + r;
+      if (p >= n) continue;
+      float *dst = GX2 + p * Dp + b0 + wn * 64 + i;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) dst[ni * 16] += acc[mi][ni][r];
     }
 }
 
@@ -906,6 +1080,129 @@ __global__ void __launch_bounds__(256) web_wgrad_kernel(const float *__restrict_
       float *dst = base + (size_t)a * Dp + b0 + wn * 64 + i;
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) dst[ni * 16] += T.c[mi][ni][r];
+    }
+}
+
+// ---- gWs on bf16 MFMAs: the contraction runs over pairs, so the operands are staged
+// transposed ([a][p] and [b][p], pairs contiguous): thread (column c, half h) loads the
+// column of 16 pairs of one active 16-pair chunk (two active chunks per 32-deep step,
+// any two: the k-slots are only summed), splits them and writes 32 bytes per part ----
+__global__ void __launch_bounds__(256) web_wgrad_kernel_b3(const float *__restrict__ X1,
+                                                           const float *__restrict__ X2,
+                                                           const float *__restrict__ GM,
+                                                           const int2 *__restrict__ ext16,
+                                                           int64_t n, int Dp, int K,
+                                                           float *__restrict__ GWS) {
+  __shared__ __attribute__((aligned(16))) uint16_t sA[3 * B3PART], sB[3 * B3PART];
+  __shared__ int act[1024];
+  __shared__ int wcnt[4];
+  const int nbt = Dp / TB;
+  const int a0 = (blockIdx.x / nbt) * TB, b0 = (blockIdx.x % nbt) * TB;
+  const int k = blockIdx.y, s = blockIdx.z;
+  const int64_t nc = (n + 15) / 16;
+  const int64_t c0 = nc * s / WSPLIT, c1 = nc * (s + 1) / WSPLIT;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, i = l & 15, g = l >> 4;
+  const int wm = w >> 1, wn = w & 1;
+  const int col = tid & 127, half = tid >> 7;
+  // raw prefetch registers (the gm scaling happens at the LDS store, so the loads of
+  // the next step stay in flight during this step's MFMAs)
+  float xg[16], xa[16], xb[16];
+  auto stage = [&](int64_t c) {   // c < 0: a zero chunk
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t p = c * 16 + r;
+      xg[r] = xa[r] = xb[r] = 0.f;
+      if (c >= 0 && p < n) {
+        xg[r] = GM[p * WKP + k];
+        xa[r] = X1[p * Dp + a0 + col];
+        xb[r] = X2[p * Dp + b0 + col];
+      }
+    }
+  };
+  auto put = [&](uint16_t *plane, const float (&x)[16], bool scale) {
+    uint32_t h[8], m[8], lo[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float v0 = scale ? xg[2 * q] * x[2 * q] : x[2 * q];
+      const float v1 = scale ? xg[2 * q + 1] * x[2 * q + 1] : x[2 * q + 1];
+      sgk::split3(v0, v1, h[q], m[q], lo[q]);
+    }
+    uint16_t *d = plane + col * B3S + 16 * half;
+    *(uint4 *)d = uint4{h[0], h[1], h[2], h[3]};
+    *(uint4 *)(d + 8) = uint4{h[4], h[5], h[6], h[7]};
+    *(uint4 *)(d + B3PART) = uint4{m[0], m[1], m[2], m[3]};
+    *(uint4 *)(d + B3PART + 8) = uint4{m[4], m[5], m[6], m[7]};
+    *(uint4 *)(d + 2 * B3PART) = uint4{lo[0], lo[1], lo[2], lo[3]};
+    *(uint4 *)(d + 2 * B3PART + 8) = uint4{lo[4], lo[5], lo[6], lo[7]};
+  };
+  f4 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t wbase = c0; wbase < c1; wbase += 1024) {
+    int na = 0;
+    for (int r0 = 0; r0 < 1024 && wbase + r0 < c1; r0 += 256) {
+      const int64_t c = wbase + r0 + tid;
+      bool on = false;
+      if (c < c1) {
+        const int2 e = ext16[c];
+        on = e.x > a0 && e.y > b0;
+      }
+      const uint64_t bal = __ballot(on);
+      const int before = __popcll(bal & ((1ull << l) - 1ull));
+      if (l == 0) wcnt[w] = __popcll(bal);
+      __syncthreads();
+      int off = na;
+      for (int u = 0; u < w; ++u) off += wcnt[u];
+      if (on) act[off + before] = (int)(r0 + tid);
+      na += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+      __syncthreads();
+    }
+    if (na == 0) continue;
+    const int nsteps = (na + 1) / 2;
+    auto chunk_of = [&](int x) -> int64_t {   // this thread's chunk of 32-deep step x
+      const int j = 2 * x + half;
+      return j < na ? wbase + act[j] : (int64_t)-1;
+    };
+    stage(chunk_of(0));
+    for (int x = 0; x < nsteps; ++x) {
+      put(sA, xa, true);
+      put(sB, xb, false);
+      __syncthreads();
+      if (x + 1 < nsteps) stage(chunk_of(x + 1));
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int oa = (wm * 64 + mi * 16 + i) * B3S + 8 * g;
+        const uint4 ah = *(const uint4 *)(sA + oa), am = *(const uint4 *)(sA + B3PART + oa),
+                    al = *(const uint4 *)(sA + 2 * B3PART + oa);
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const int ob = (wn * 64 + ni * 16 + i) * B3S + 8 * g;
+          const uint4 bh = *(const uint4 *)(sB + ob), bm = *(const uint4 *)(sB + B3PART + ob),
+                      bl = *(const uint4 *)(sB + 2 * B3PART + ob);
+          f4 c = acc[mi][ni];
+          c = sgk::mfbf(al, bh, c);
+          c = sgk::mfbf(ah, bl, c);
+          c = sgk::mfbf(am, bm, c);
+          c = sgk::mfbf(am, bh, c);
+          c = sgk::mfbf(ah, bm, c);
+          c = sgk::mfbf(ah, bh, c);
+          acc[mi][ni] = c;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  float *base = GWS + (((size_t)s * K + k) * Dp) * Dp;
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int a = a0 + wm * 64 + mi * 16 + 4 * g + r;
+      float *dst = base + (size_t)a * Dp + b0 + wn * 64 + i;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) dst[ni * 16] += acc[mi][ni][r];
     }
 }
 
@@ -1290,19 +1587,30 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     G.n_pairs = n;
     G.pair_offset = pair_offset + c0;
     if ((rc = gcn_launch(false, W, G, 2 * n, st)) != SG_OK) return rc;
-    hipLaunchKernelGGL(web_t_kernel, dim3((unsigned)nblk, Dp / TB, K), dim3(256), 0, st,
-                       X + ws.Cp * Dp, Wg,
-                       EXT128, n, Dp, K, T);
+    if (SG_WEB_T_BF3)
+      hipLaunchKernelGGL(web_t_kernel_b3, dim3((unsigned)nblk, Dp / TB, K), dim3(256), 0, st,
+                         X + ws.Cp * Dp, Wg, EXT128, n, Dp, K, T);
+    else
+      hipLaunchKernelGGL(web_t_kernel, dim3((unsigned)nblk, Dp / TB, K), dim3(256), 0, st,
+                         X + ws.Cp * Dp, Wg, EXT128, n, Dp, K, T);
     H.n = n;
     H.labels = labels ? labels + c0 : nullptr;
     H.s_out = s_out ? s_out + c0 : nullptr;
     const int hb = (int)((n + 3) / 4 < ws.head_blocks ? (n + 3) / 4 : ws.head_blocks);
     if (bwd) {
       hipLaunchKernelGGL(web_head_kernel<true>, dim3(hb), dim3(256), head_lds, st, H);
-      hipLaunchKernelGGL(web_gx2_kernel, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, st, X, GM,
-                         Wh, EXT128, n, Dp, K, GX + ws.Cp * Dp);
-      hipLaunchKernelGGL(web_wgrad_kernel, dim3((Dp / TB) * (Dp / TB), K, WSPLIT), dim3(256), 0,
-                         st, X, X + ws.Cp * Dp, GM, EXT16, n, Dp, K, GWS);
+      if (SG_WEB_T_BF3)
+        hipLaunchKernelGGL(web_gx2_kernel_b3, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, st, X,
+                           GM, Wh, EXT128, n, Dp, K, GX + ws.Cp * Dp);
+      else
+        hipLaunchKernelGGL(web_gx2_kernel, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, st, X, GM,
+                           Wh, EXT128, n, Dp, K, GX + ws.Cp * Dp);
+      if (SG_WEB_T_BF3)
+        hipLaunchKernelGGL(web_wgrad_kernel_b3, dim3((Dp / TB) * (Dp / TB), K, WSPLIT), dim3(256),
+                           0, st, X, X + ws.Cp * Dp, GM, EXT16, n, Dp, K, GWS);
+      else
+        hipLaunchKernelGGL(web_wgrad_kernel, dim3((Dp / TB) * (Dp / TB), K, WSPLIT), dim3(256), 0,
+                           st, X, X + ws.Cp * Dp, GM, EXT16, n, Dp, K, GWS);
       hipLaunchKernelGGL(web_gv_kernel, dim3(2 * Dp / 64, WSPLIT), dim3(256), 0, st, X, GM, n,
                          ws.Cp, Dp, K, GVS);
       if ((rc = gcn_launch(true, W, G, 2 * n, st)) != SG_OK) return rc;
