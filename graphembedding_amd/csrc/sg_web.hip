@@ -1089,15 +1089,19 @@ __global__ void __launch_bounds__(256) web_wgrad_kernel(const float *__restrict_
 // transposed ([a][p] and [b][p], pairs contiguous): thread (column c, half h) loads the
 // column of 16 pairs of one active 16-pair chunk (two active chunks per 32-deep step,
 // any two: the k-slots are only summed), splits them and writes 32 bytes per part ----
+// It also forms gV = gmᵀ [x1 | x2] (web_gv_kernel's sums) from the operands it stages:
+// the blocks of b-tile 0 sum gm·x1 over their columns a, those of a-tile 0 gm·x2 over b.
 __global__ void __launch_bounds__(256) web_wgrad_kernel_b3(const float *__restrict__ X1,
                                                            const float *__restrict__ X2,
                                                            const float *__restrict__ GM,
                                                            const int2 *__restrict__ ext16,
                                                            int64_t n, int Dp, int K,
-                                                           float *__restrict__ GWS) {
+                                                           float *__restrict__ GWS,
+                                                           float *__restrict__ GVS) {
   __shared__ __attribute__((aligned(16))) uint16_t sA[3 * B3PART], sB[3 * B3PART];
   __shared__ int act[1024];
   __shared__ int wcnt[4];
+  __shared__ float gvh[2][TB];
   const int nbt = Dp / TB;
   const int a0 = (blockIdx.x / nbt) * TB, b0 = (blockIdx.x % nbt) * TB;
   const int k = blockIdx.y, s = blockIdx.z;
@@ -1121,6 +1125,8 @@ __global__ void __launch_bounds__(256) web_wgrad_kernel_b3(const float *__restri
       }
     }
   };
+  const bool gv1 = (blockIdx.x % nbt) == 0, gv2 = (blockIdx.x / nbt) == 0;
+  float gva = 0.f, gvb = 0.f;   // Σ gm·x1[a0 + col], Σ gm·x2[b0 + col] over this thread's pairs
   auto put = [&](uint16_t *plane, const float (&x)[16], bool scale) {
     uint32_t h[8], m[8], lo[8];
 #pragma unroll
@@ -1128,6 +1134,14 @@ __global__ void __launch_bounds__(256) web_wgrad_kernel_b3(const float *__restri
       const float v0 = scale ? xg[2 * q] * x[2 * q] : x[2 * q];
       const float v1 = scale ? xg[2 * q + 1] * x[2 * q + 1] : x[2 * q + 1];
       sgk::split3(v0, v1, h[q], m[q], lo[q]);
+    }
+    if (scale && gv1) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gva = fmaf(xg[r], x[r], gva);
+    }
+    if (!scale && gv2) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) gvb = fmaf(xg[r], x[r], gvb);
     }
     uint16_t *d = plane + col * B3S + 16 * half;
     *(uint4 *)d = uint4{h[0], h[1], h[2], h[3]};
@@ -1206,6 +1220,18 @@ __global__ void __launch_bounds__(256) web_wgrad_kernel_b3(const float *__restri
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) dst[ni * 16] += acc[mi][ni][r];
     }
+  if (gv1 || gv2) {   // the two halves' sums, half 0 first (fixed order)
+    if (half) {
+      gvh[0][col] = gva;
+      gvh[1][col] = gvb;
+    }
+    __syncthreads();
+    if (!half) {
+      float *gv = GVS + ((size_t)s * WKP + k) * 2 * Dp;
+      if (gv1) gv[a0 + col] += gva + gvh[0][col];
+      if (gv2) gv[Dp + b0 + col] += gvb + gvh[1][col];
+    }
+  }
 }
 
 // ---- gVs[s][k][c] += Σ_{p in split s} gm[p][k] x12[p][c]  (c < Dp: x1, else x2) ----
@@ -1607,14 +1633,15 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
       else
         hipLaunchKernelGGL(web_gx2_kernel, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, st, X, GM,
                            Wh, EXT128, n, Dp, K, GX + ws.Cp * Dp);
-      if (SG_WEB_T_BF3)
+      if (SG_WEB_T_BF3) {   // gV rides along
         hipLaunchKernelGGL(web_wgrad_kernel_b3, dim3((Dp / TB) * (Dp / TB), K, WSPLIT), dim3(256),
-                           0, st, X, X + ws.Cp * Dp, GM, EXT16, n, Dp, K, GWS);
-      else
+                           0, st, X, X + ws.Cp * Dp, GM, EXT16, n, Dp, K, GWS, GVS);
+      } else {
         hipLaunchKernelGGL(web_wgrad_kernel, dim3((Dp / TB) * (Dp / TB), K, WSPLIT), dim3(256), 0,
                            st, X, X + ws.Cp * Dp, GM, EXT16, n, Dp, K, GWS);
-      hipLaunchKernelGGL(web_gv_kernel, dim3(2 * Dp / 64, WSPLIT), dim3(256), 0, st, X, GM, n,
-                         ws.Cp, Dp, K, GVS);
+        hipLaunchKernelGGL(web_gv_kernel, dim3(2 * Dp / 64, WSPLIT), dim3(256), 0, st, X, GM, n,
+                           ws.Cp, Dp, K, GVS);
+      }
       if ((rc = gcn_launch(true, W, G, 2 * n, st)) != SG_OK) return rc;
     } else {
       hipLaunchKernelGGL(web_head_kernel<false>, dim3(hb), dim3(256), head_lds, st, H);
