@@ -795,11 +795,17 @@ __device__ __forceinline__ void b3_split_store(uint16_t *plane, int r, int c, fl
   *(uint2 *)(plane + 2 * B3PART + o) = uint2{l01, l23};
 }
 
+// MFUSE: instead of T, write the tile's share of the bilinear term,
+// MP[p][k][a-tile] = Σ_{a in the tile} x1[p][a] T[p][k][a] (T itself never reaches memory:
+// the head sums the a-tiles, and gx1's T term is a GEMM of its own, web_gx1_kernel_b3)
+template <bool MFUSE>
 __global__ void __launch_bounds__(256) web_t_kernel_b3(const float *__restrict__ X2,
                                                        const float *__restrict__ Wg,
                                                        const int2 *__restrict__ ext128, int64_t n,
-                                                       int Dp, int K, float *__restrict__ Tout) {
+                                                       int Dp, int K, float *__restrict__ Tout,
+                                                       const float *__restrict__ X1) {
   __shared__ __attribute__((aligned(16))) uint16_t sA[3 * B3PART], sB[3 * B3PART];
+  __shared__ float mred[2][TB];
   const int64_t p0 = (int64_t)blockIdx.x * TB;
   const int a0 = blockIdx.y * TB, k = blockIdx.z;
   const int2 e = ext128[blockIdx.x];
@@ -854,6 +860,25 @@ __global__ void __launch_bounds__(256) web_t_kernel_b3(const float *__restrict__
       }
     }
     __syncthreads();
+  }
+  if (MFUSE) {
+    // lane (i, g): rows 4g + r of each 16-row group, columns 16 ni + i of the wave's half
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int pl = wm * 64 + mi * 16 + 4 * g + r;
+        const float *x1 = X1 + (p0 + pl) * Dp + a0 + wn * 64 + i;
+        float part = 0.f;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) part = fmaf(x1[ni * 16], acc[mi][ni][r], part);
+        part = sgk::row_sum16(part);
+        if (i == 0) mred[wn][pl] = part;
+      }
+    __syncthreads();
+    if (tid < TB && p0 + tid < n)
+      Tout[((p0 + tid) * WKP + k) * 4 + blockIdx.y] = mred[0][tid] + mred[1][tid];
+    return;
   }
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
@@ -1085,6 +1110,86 @@ __global__ void __launch_bounds__(256) web_wgrad_kernel(const float *__restrict_
     }
 }
 
+// ---- the T term of gX1 as a GEMM (with web_t_kernel_b3<true>, T is never stored):
+// gX1[p][a] += Σ_{k,b} gm[p][k] x2[p][b] W[a][b][k]; A = gm·x2 scaled while staging,
+// B = Wg[k][a][b]; 32-deep chunks of b for each k ----
+__global__ void __launch_bounds__(256) web_gx1_kernel_b3(const float *__restrict__ X2,
+                                                         const float *__restrict__ GM,
+                                                         const float *__restrict__ Wg,
+                                                         const int2 *__restrict__ ext128,
+                                                         int64_t n, int Dp, int K,
+                                                         float *__restrict__ GX1) {
+  __shared__ __attribute__((aligned(16))) uint16_t sA[3 * B3PART], sB[3 * B3PART];
+  const int64_t p0 = (int64_t)blockIdx.x * TB;
+  const int a0 = blockIdx.y * TB;
+  const int2 e = ext128[blockIdx.x];
+  if (a0 >= e.x) return;
+  const int nb = (e.y + B3K - 1) / B3K * B3K;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, i = l & 15, g = l >> 4;
+  const int wm = w >> 1, wn = w & 1;
+  float4 ra[4], rb[4];
+  float gmr[4];
+  auto load = [&](int k, int b0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = tid + 256 * u, r = q >> 3, c = (q & 7) * 4;
+      const int64_t p = p0 + r;
+      gmr[u] = p < n ? GM[p * WKP + k] : 0.f;
+      ra[u] = *(const float4 *)(X2 + p * Dp + b0 + c);
+      rb[u] = *(const float4 *)(Wg + ((size_t)k * Dp + a0 + r) * Dp + b0 + c);
+    }
+  };
+  f4 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f4{0.f, 0.f, 0.f, 0.f};
+  const int steps = nb / B3K, total = K * steps;
+  if (total > 0) load(0, 0);
+  for (int st = 0; st < total; ++st) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = tid + 256 * u, r = q >> 3, c = (q & 7) * 4;
+      const float gm = gmr[u];
+      b3_split_store(sA, r, c, make_float4(gm * ra[u].x, gm * ra[u].y, gm * ra[u].z, gm * ra[u].w));
+      b3_split_store(sB, r, c, rb[u]);
+    }
+    __syncthreads();
+    if (st + 1 < total) load((st + 1) / steps, ((st + 1) % steps) * B3K);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int oa = (wm * 64 + mi * 16 + i) * B3S + 8 * g;
+      const uint4 ah = *(const uint4 *)(sA + oa), am = *(const uint4 *)(sA + B3PART + oa),
+                  al = *(const uint4 *)(sA + 2 * B3PART + oa);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int ob = (wn * 64 + ni * 16 + i) * B3S + 8 * g;
+        const uint4 bh = *(const uint4 *)(sB + ob), bm = *(const uint4 *)(sB + B3PART + ob),
+                    bl = *(const uint4 *)(sB + 2 * B3PART + ob);
+        f4 c = acc[mi][ni];
+        c = sgk::mfbf(al, bh, c);
+        c = sgk::mfbf(ah, bl, c);
+        c = sgk::mfbf(am, bm, c);
+        c = sgk::mfbf(am, bh, c);
+        c = sgk::mfbf(ah, bm, c);
+        c = sgk::mfbf(ah, bh, c);
+        acc[mi][ni] = c;
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t p = p0 + wm * 64 + mi * 16 + 4 * g + r;
+      if (p >= n) continue;
+      float *dst = GX1 + p * Dp + a0 + wn * 64 + i;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) dst[ni * 16] += acc[mi][ni][r];
+    }
+}
+
 // ---- gWs on bf16 MFMAs: the contraction runs over pairs, so the operands are staged
 // transposed ([a][p] and [b][p], pairs contiguous): thread (column c, half h) loads the
 // column of 16 pairs of one active 16-pair chunk (two active chunks per 32-deep step,
@@ -1276,6 +1381,7 @@ __global__ void __launch_bounds__(256) web_gv_kernel(const float *__restrict__ X
 struct HeadArgs {
   const float *X, *T, *params, *labels, *y_stats;
   const int2 *ext;
+  const int2 *ext128;   // MT: per-128-pair extents (which a-tiles web_t_kernel_b3 computed)
   float *GX, *GM, *s_out, *hslab;
   int64_t n, Cp;
   int D, Dp, K, oV, oU, obn;
@@ -1283,7 +1389,9 @@ struct HeadArgs {
   float yeta, inv_batch;
 };
 
-template <bool BWD>
+// MT: T holds web_t_kernel_b3<true>'s a-tile shares MP[p][k][tile] of Σ_a x1[a] T[k][a]
+// instead of T, and gx1 gets only its V term here (web_gx1_kernel_b3 adds the T term)
+template <bool BWD, bool MT>
 __global__ void __launch_bounds__(256) web_head_kernel(HeadArgs A) {
   extern __shared__ __attribute__((aligned(16))) float sV[];   // [K][2Dp]: V[k][a] | V[k][D+b]
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
@@ -1319,17 +1427,28 @@ __global__ void __launch_bounds__(256) web_head_kernel(HeadArgs A) {
 #pragma unroll
       for (int k = 0; k < WKP; ++k) {
         if (k < K) {
-          const float t = a < e1 ? Tp[k * Dp + a] : 0.f;
+          const float t = (!MT && a < e1) ? Tp[k * Dp + a] : 0.f;
           m[k] = fmaf(xa, t + sV[k * 2 * Dp + a], m[k]);
           m[k] = fmaf(xb, sV[k * 2 * Dp + Dp + a], m[k]);
         }
       }
     }
+    float mt[WKP];   // MT: the bilinear term from the a-tile shares, tiles in order
+#pragma unroll
+    for (int k = 0; k < WKP; ++k) mt[k] = 0.f;
+    if (MT) {
+      const int ex = A.ext128[p / TB].x;
+      const float *mp = A.T + (size_t)p * WKP * 4;
+#pragma unroll
+      for (int k = 0; k < WKP; ++k)
+        if (k < K)
+          for (int t = 0; t < 4 && t * TB < ex; ++t) mt[k] += mp[k * 4 + t];
+    }
     float rsum = 0.f, s = 0.f;
 #pragma unroll
     for (int k = 0; k < WKP; ++k) {
       if (k < K) {
-        m[k] = sg_wave_sum(m[k]) + bn[k];
+        m[k] = sg_wave_sum(m[k]) + mt[k] + bn[k];
         const float r = m[k] > 0.f ? m[k] : 0.f;
         rsum += r;
         s = fmaf(U[k], r, s);
@@ -1375,7 +1494,7 @@ __global__ void __launch_bounds__(256) web_head_kernel(HeadArgs A) {
 #pragma unroll
       for (int k = 0; k < WKP; ++k) {
         if (k < K) {
-          const float t = a < e1 ? Tp[k * Dp + a] : 0.f;
+          const float t = (!MT && a < e1) ? Tp[k * Dp + a] : 0.f;
           v1 = fmaf(gm[k], t + sV[k * 2 * Dp + a], v1);
           v2 = fmaf(gm[k], sV[k * 2 * Dp + Dp + a], v2);
         }
@@ -1596,7 +1715,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
   G.ob0 = W.ob0; G.oW1 = W.oW1; G.ob1 = W.ob1; G.oWd = W.oWd; G.obd = W.obd;
   HeadArgs H;
   H.X = X; H.T = T; H.params = params; H.labels = labels; H.y_stats = y_stats;
-  H.ext = EXT; H.GX = GX; H.GM = GM; H.s_out = nullptr; H.hslab = HS;
+  H.ext = EXT; H.ext128 = EXT128; H.GX = GX; H.GM = GM; H.s_out = nullptr; H.hslab = HS;
   H.Cp = ws.Cp; H.D = D; H.Dp = Dp; H.K = K; H.oV = W.oV; H.oU = W.oU; H.obn = W.obn;
   H.final_act = W.final_act; H.loss_mode = W.loss_mode; H.ntn_mode = W.ntn_mode;
   H.yeta = W.yeta;
@@ -1616,8 +1735,8 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     G.pair_offset = pair_offset + c0;
     if ((rc = gcn_launch(false, W, G, 2 * n, st)) != SG_OK) return rc;
     if (SG_WEB_T_BF3)
-      hipLaunchKernelGGL(web_t_kernel_b3, dim3((unsigned)nblk, Dp / TB, K), dim3(256), 0, st,
-                         X + ws.Cp * Dp, Wg, EXT128, n, Dp, K, T);
+      hipLaunchKernelGGL(web_t_kernel_b3<true>, dim3((unsigned)nblk, Dp / TB, K), dim3(256), 0,
+                         st, X + ws.Cp * Dp, Wg, EXT128, n, Dp, K, T, X);
     else
       hipLaunchKernelGGL(web_t_kernel, dim3((unsigned)nblk, Dp / TB, K), dim3(256), 0, st,
                          X + ws.Cp * Dp, Wg, EXT128, n, Dp, K, T);
@@ -1626,13 +1745,17 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     H.s_out = s_out ? s_out + c0 : nullptr;
     const int hb = (int)((n + 3) / 4 < ws.head_blocks ? (n + 3) / 4 : ws.head_blocks);
     if (bwd) {
-      hipLaunchKernelGGL(web_head_kernel<true>, dim3(hb), dim3(256), head_lds, st, H);
-      if (SG_WEB_T_BF3)
+      if (SG_WEB_T_BF3) {
+        hipLaunchKernelGGL((web_head_kernel<true, true>), dim3(hb), dim3(256), head_lds, st, H);
+        hipLaunchKernelGGL(web_gx1_kernel_b3, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, st,
+                           X + ws.Cp * Dp, GM, Wg, EXT128, n, Dp, K, GX);
         hipLaunchKernelGGL(web_gx2_kernel_b3, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, st, X,
                            GM, Wh, EXT128, n, Dp, K, GX + ws.Cp * Dp);
-      else
+      } else {
+        hipLaunchKernelGGL((web_head_kernel<true, false>), dim3(hb), dim3(256), head_lds, st, H);
         hipLaunchKernelGGL(web_gx2_kernel, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, st, X, GM,
                            Wh, EXT128, n, Dp, K, GX + ws.Cp * Dp);
+      }
       if (SG_WEB_T_BF3) {   // gV rides along
         hipLaunchKernelGGL(web_wgrad_kernel_b3, dim3((Dp / TB) * (Dp / TB), K, WSPLIT), dim3(256),
                            0, st, X, X + ws.Cp * Dp, GM, EXT16, n, Dp, K, GWS, GVS);
@@ -1644,7 +1767,10 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
       }
       if ((rc = gcn_launch(true, W, G, 2 * n, st)) != SG_OK) return rc;
     } else {
-      hipLaunchKernelGGL(web_head_kernel<false>, dim3(hb), dim3(256), head_lds, st, H);
+      if (SG_WEB_T_BF3)
+        hipLaunchKernelGGL((web_head_kernel<false, true>), dim3(hb), dim3(256), head_lds, st, H);
+      else
+        hipLaunchKernelGGL((web_head_kernel<false, false>), dim3(hb), dim3(256), head_lds, st, H);
     }
   }
   if (!bwd) return web_status();
