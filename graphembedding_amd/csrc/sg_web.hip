@@ -248,9 +248,8 @@ __global__ void __launch_bounds__(256) web_wprep_h(const float *__restrict__ Wg,
 // ---------------------------------------------------------------------------
 // Per-instance GCN → Dense → Padding stack (+ backward with recompute).
 // One workgroup per instance (pair, side); node tiles of 16 rows, tile t on wave
-// t % waves (N <= 512: 32 tiles).  The instance's CSR rows
-// are staged in LDS when they fit (one coalesced copy, then ~100-cycle reads in
-// the sparse loops instead of a dependent global-load chain per neighbour).
+// t % waves (N <= 512: 32 tiles).  The sparse loops read the instance's CSR rows
+// through the caches; LCSR (opt-in) stages them in LDS first.
 // ---------------------------------------------------------------------------
 // waves per instance workgroup: 16 forward (2 tiles per wave), SG_WEB_BWD_WAVES backward.
 // The backward wants more than the 128 VGPRs of a 16-wave block and spills ~32 of them
@@ -1600,7 +1599,7 @@ static int web_status() {
   return SG_ERR_HIP;
 }
 
-// LDS of the instance kernel; CSR staged in LDS when it fits
+// LDS of the instance kernel (+ the CSR rows with LCSR)
 static size_t gcn_lds_bytes(const WebPlan &W, int n_max, int max_nnz, bool bwd, bool lcsr) {
   const int n16 = (n_max + 15) & ~15;
   const GcnLds L = gcn_lds(W.d_in, n16, max_nnz, bwd, lcsr);
@@ -1614,7 +1613,11 @@ static size_t gcn_lds_bytes(const WebPlan &W, int n_max, int max_nnz, bool bwd, 
 
 static int gcn_launch(bool bwd, const WebPlan &W, const GcnArgs &A, int64_t n_inst,
                       hipStream_t st) {
-  const bool lcsr = gcn_lds_bytes(W, A.n_max, A.max_nnz, bwd, true) <= 163840u &&
+  // CSR rows staged in LDS (LCSR) measured slower than reading them through the caches
+  // once the instance kernels run 16 waves (forward 14.7 -> 13.1 ms per chunk without),
+  // so it is opt-in (SG_WEB_LCSR=1); the backward's LDS no longer fits it at 16 waves
+  static const bool want_lcsr = getenv("SG_WEB_LCSR") != nullptr;
+  const bool lcsr = want_lcsr && gcn_lds_bytes(W, A.n_max, A.max_nnz, bwd, true) <= 163840u &&
                     A.max_nnz <= 4096;
   const size_t lds = gcn_lds_bytes(W, A.n_max, A.max_nnz, bwd, lcsr);
   if (lds > 163840u) return SG_ERR_UNSUPPORTED;
