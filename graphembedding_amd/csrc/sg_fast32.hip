@@ -258,9 +258,23 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
   }
   int pnext = (ord && slot_of(0) < npairs) ? ord_at(ordA, 0) : slot_of(0);
 
+  // wave priority as sg_fast: waves w and w ^ 4 share a SIMD; the higher priority
+  // alternates between them by pair count so that neither finishes far ahead
+#ifndef SG_PRIO32_PERIOD
+#define SG_PRIO32_PERIOD 3
+#endif
+#ifndef SG_PRIO32_YOUNG
+#define SG_PRIO32_YOUNG 2
+#endif
+  const bool young = wv >= 4;
   for (int it = 0;; ++it) {
     const int q = slot_of(it);
     if (q >= npairs) break;
+    if (SG_PRIO32_PERIOD > 0) {
+      const bool yturn = (it % SG_PRIO32_PERIOD) < SG_PRIO32_YOUNG;
+      if (yturn == young) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
     const int p = pnext;
     // ---- stage the record (f32 LDS image; bf16 Â widened) ----
     {
