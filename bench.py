@@ -59,6 +59,9 @@ def parse():
     p.add_argument('--stack', choices=('default', 'average'), default='default',
                    help="layer stack: the default config.py:44-66 stack, or tuning.py:66-93's "
                         "GCN-GCN-Average-NTN(16)")
+    p.add_argument('--collective', choices=('rccl', 'torch'), default='rccl',
+                   help='N > 1: the gradient all-reduce as ncclAllReduce on the compute stream '
+                        '(rccl) or through torch.distributed (side stream + events)')
     p.add_argument('--json-out', default='')
     p.add_argument('--emulate-world', type=int, default=0,
                    help='diagnostic: time rank 0\'s share of a W-GPU step on one GPU (no collective)')
@@ -140,7 +143,7 @@ def main():
     from graphembedding_amd.allpairs import AllPairsShard, AllPairsStream, load_graph_set
     from graphembedding_amd.config import Flags
     from graphembedding_amd.model_mse import SiameseGCNTNMSE
-    from graphembedding_amd.shard import make_allreduce_hook
+    from graphembedding_amd.shard import make_allreduce_hook, make_rccl_hook
 
     c4 = args.dataset == 'syn_aids10knef'
     D = 512 if web else (30 if c4 else 10)
@@ -191,7 +194,23 @@ def main():
                                            grid_base=shard.start, pair_offset=shard.start,
                                            batch_total=shard.total, y_stats=batch.y_stats)
             batch = model.balance(batch) if balance else batch
-    hook = make_allreduce_hook() if world > 1 else None
+    hook, collective = None, None
+    if world > 1:
+        # RCCL on the compute stream, in order with the fused kernels (no side stream, no
+        # cross-stream events: 8 us less per step than torch.distributed's RCCL call,
+        # scripts/collective_overhead.py); torch.distributed for the gloo rehearsal
+        collective = 'torch' if rehearsal else args.collective
+        if collective == 'rccl':
+            from graphembedding_amd.rccl import RcclComm
+            try:
+                comm = RcclComm(rank, world)
+                hook = make_rccl_hook(comm)
+            except RuntimeError as e:   # every rank fails alike (library / init), so all fall back
+                print('bench.py: direct RCCL unavailable ({}); torch.distributed all-reduce'.format(e),
+                      file=sys.stderr, flush=True)
+                collective = 'torch'
+        if collective == 'torch':
+            hook = make_allreduce_hook()
     if not web:
         model.workspace(shard.chunk if streamed else batch.n_pairs)
     stream = torch.cuda.current_stream()
@@ -326,7 +345,11 @@ def main():
                        'records': records,
                        'order': 'size buckets' if web else args.order,
                        'inputs': inputs,
-                       'parallelism': 'dp{}'.format(world)},
+                       'parallelism': 'dp{}'.format(world),
+                       'collective': ('{} all-reduce of the flat gradient + loss ({} B)'.format(
+                           'ncclAllReduce on the compute stream' if collective == 'rccl' else
+                           'torch.distributed', 4 * (model.grad.numel() + 1))
+                           if collective else None)},
             'roofline': {'bound': 'mfma', 'achieved': achieved_tf, 'peak': FP32_PEAK_TFLOPS,
                          'unit': 'TFLOP/s', 'frac': achieved_tf / FP32_PEAK_TFLOPS,
                          'traffic': traffic,
@@ -349,6 +372,8 @@ def main():
             with open(args.json_out, 'w') as f:
                 f.write(line + '\n')
     if world > 1:
+        if collective == 'rccl':
+            comm.destroy()
         dist.destroy_process_group()
 
 

@@ -37,3 +37,17 @@ def make_allreduce_hook(group=None):
         model.loss_buf[:1].copy_(tmp[n:])
 
     return hook
+
+
+def make_rccl_hook(comm):
+    """Model.grad_hook over a rccl.RcclComm: the same in-place SUM of grad | loss_mse,
+    enqueued by RCCL directly on the compute stream (no side stream, no events)."""
+
+    def hook(model):
+        n = model.grad.numel()
+        buf = model.grad_loss
+        if model.grad.data_ptr() != buf.data_ptr() or model.loss_buf.data_ptr() != buf[n:].data_ptr():
+            raise RuntimeError('make_rccl_hook: grad and loss_buf must be views of grad_loss')
+        comm.all_reduce_sum_(buf[:n + 1])
+
+    return hook

@@ -11,7 +11,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from graphembedding_amd.shard import make_allreduce_hook, shard_range
+from graphembedding_amd.shard import make_allreduce_hook, make_rccl_hook, shard_range
 
 
 def test_shard_range_partitions():
@@ -90,3 +90,26 @@ def test_two_rank_gloo_step_equals_single_process(shared):
     for rank, err, lerr, scale in out:
         assert err <= 1e-5 * max(1.0, scale), (rank, err)
         assert lerr <= 1e-4, (rank, lerr)
+
+
+def test_rccl_hook_reduces_grad_loss_in_place():
+    """shard.make_rccl_hook hands the collective exactly grad | loss_mse (one in-place
+    call on the shared buffer) and refuses a model whose buffers are not views of it."""
+    calls = []
+
+    class _Comm:
+        def all_reduce_sum_(self, t):
+            calls.append(t)
+            t.mul_(2.0)
+
+    m = _FakeModel([1.0, -2.0, 3.0], 0.5, shared=True)
+    hook = make_rccl_hook(_Comm())
+    hook(m)
+    assert len(calls) == 1 and calls[0].numel() == 4
+    assert calls[0].data_ptr() == m.grad_loss.data_ptr()
+    assert m.grad.tolist() == [2.0, -4.0, 6.0] and float(m.loss_buf[0]) == 1.0
+    assert float(m.loss_buf[1]) == 0.0
+    with pytest.raises(RuntimeError):
+        m2 = _FakeModel([1.0], 0.0, shared=False)
+        m2.grad_loss = torch.zeros(3)
+        hook(m2)
