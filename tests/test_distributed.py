@@ -113,3 +113,18 @@ def test_rccl_hook_reduces_grad_loss_in_place():
         m2 = _FakeModel([1.0], 0.0, shared=False)
         m2.grad_loss = torch.zeros(3)
         hook(m2)
+
+
+def test_rccl_binding_loads():
+    """graphembedding_amd.rccl binds torch's own librccl.so (the symbols the direct
+    collective uses) and draws a unique id without touching a GPU."""
+    import ctypes
+    from graphembedding_amd.rccl import NCCL_UNIQUE_ID_BYTES, _UniqueId, _rccl
+    L = _rccl()
+    for sym in ('ncclGetUniqueId', 'ncclCommInitRank', 'ncclAllReduce', 'ncclCommDestroy',
+                'ncclGetErrorString'):
+        assert hasattr(L, sym), sym
+    uid = _UniqueId()
+    assert L.ncclGetUniqueId(ctypes.byref(uid)) == 0
+    assert ctypes.sizeof(uid) == NCCL_UNIQUE_ID_BYTES
+    assert any(ctypes.string_at(ctypes.addressof(uid), NCCL_UNIQUE_ID_BYTES))
