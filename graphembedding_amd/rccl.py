@@ -66,10 +66,15 @@ class RcclComm(object):
     call after torch.cuda.set_device).  `store` is any torch.distributed Store reachable
     by every rank; default: the default process group's store."""
 
-    def __init__(self, rank: int, world: int, store=None, tag: str = 'sg_rccl_uid'):
+    _count = 0   # communicators opened by this process: every rank opens them in the same order
+
+    def __init__(self, rank: int, world: int, store=None, tag: str = None):
         import torch.distributed as dist
         if store is None:
             store = dist.distributed_c10d._get_default_store()
+        if tag is None:   # a fresh key per communicator: ranks never read a stale id
+            tag = 'sg_rccl_uid_{}'.format(RcclComm._count)
+        RcclComm._count += 1
         L = _rccl()
         uid = _UniqueId()
         if rank == 0:
