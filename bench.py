@@ -201,14 +201,17 @@ def main():
         # scripts/collective_overhead.py); torch.distributed for the gloo rehearsal
         collective = 'torch' if rehearsal else args.collective
         if collective == 'rccl':
-            from graphembedding_amd.rccl import RcclComm
-            try:
-                comm = RcclComm(rank, world)
-                hook = make_rccl_hook(comm)
-            except RuntimeError as e:   # every rank fails alike (library / init), so all fall back
-                print('bench.py: direct RCCL unavailable ({}); torch.distributed all-reduce'.format(e),
-                      file=sys.stderr, flush=True)
+            # every rank opens the communicator or none does (open_rccl agrees through the
+            # process group before and after ncclCommInitRank), so the ranks fall back to
+            # torch.distributed together and never wait on a communicator a peer abandoned
+            from graphembedding_amd.rccl import open_rccl
+            comm, why = open_rccl(rank, world)
+            if comm is None:
+                print('bench.py: direct RCCL unavailable ({}); torch.distributed all-reduce'.format(
+                    why), file=sys.stderr, flush=True)
                 collective = 'torch'
+            else:
+                hook = make_rccl_hook(comm)
         if collective == 'torch':
             hook = make_allreduce_hook()
     if not web:
@@ -248,10 +251,21 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    params_agree = None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # after timing: every rank must hold the same parameters (a wrong all-reduce
+        # would let them drift apart); max and min of a checksum over ranks
+        c = model.params.double().mul(torch.arange(1, model.params.numel() + 1, device=device,
+                                                   dtype=torch.float64)).sum()
+        ck = torch.stack([c, -c])
+        dist.all_reduce(ck, op=dist.ReduceOp.MAX)
+        params_agree = bool(float(ck[0].item()) == -float(ck[1].item()))
+        if not params_agree:
+            print('bench.py: parameters differ across ranks after the timed steps',
+                  file=sys.stderr, flush=True)
 
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     total_pairs = shard.total
@@ -277,14 +291,19 @@ def main():
         kern_pairs_s = shard.n / (kern_ms * 1e-3)
         achieved_tf = kern_pairs_s * flops_pair / 1e12
         achieved_gbs = kern_pairs_s * bytes_pair / 1e9
-        traffic = None
+        traffic, traffic_src = None, None
         tj = os.path.join(ROOT, 'profiles', 'traffic.json')
-        if model.kernel_path == 1 and args.records == 'f32' and os.path.isfile(tj):
+        if model.kernel_path == 1 and args.records == 'f32' and os.path.isfile(tj) and \
+                args.stack == 'default' and args.source != 'store':
             with open(tj) as f:
                 t = json.load(f)
-            # HBM bytes per launch from the committed PMC passes of this command
-            # (scripts/gpu_round.sh + scripts/make_profile_summary.py)
+            # HBM bytes per launch: PMC counters cannot be read from inside this process,
+            # so they come from the committed rocprofv3 --pmc passes of this same command
+            # on this tree (scripts/gpu_round3.sh + scripts/make_profile_summary.py)
             traffic = t.get('traffic_bytes_per_launch') * shard.n / 490000.0
+            traffic_src = 'profiles/{}/traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE ' \
+                          'passes of bench.py --gpus 1; FETCH_SIZE x2 gfx950 correction)'.format(
+                              t.get('tree', '?'))
         cpu = None
         if world == 1 and args.cpu_sample >= 0:
             try:
@@ -352,7 +371,7 @@ def main():
                            if collective else None)},
             'roofline': {'bound': 'mfma', 'achieved': achieved_tf, 'peak': FP32_PEAK_TFLOPS,
                          'unit': 'TFLOP/s', 'frac': achieved_tf / FP32_PEAK_TFLOPS,
-                         'traffic': traffic,
+                         'traffic': traffic, 'traffic_source': traffic_src,
                          'note': 'fp32 compute roof (gfx950 vector fp32 == f32 MFMA peak); '
                                  'algorithmic {:.0f} FLOP/pair x {} pairs per launch / {} '
                                  'event time {:.3f} ms'.format(
@@ -365,6 +384,7 @@ def main():
             'cpu_baseline': cpu,
             'forward_pairs_per_s': fwd_rate,
             'loss': loss,
+            'params_agree_across_ranks': params_agree,
         }
         line = json.dumps(out)
         print(line, flush=True)

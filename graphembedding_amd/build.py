@@ -11,15 +11,33 @@ OUT = os.path.join(_HERE, 'lib', 'libsiamese_hip.so')
 SOURCES = ['siamese_hip.hip', 'sg_generic.hip', 'sg_fast.hip', 'sg_fast32.hip',
            'sg_sampler.hip', 'sg_web.hip']
 HEADERS = ['sg_common.h', 'sg_plan.h', 'sg_mfma.h']
-ARCH = os.environ.get('SG_OFFLOAD_ARCH', 'gfx950')
+# MI355X only: the kernels use gfx950's 160 KB LDS (web_wgrad_kernel_b3 holds ≈66.6 KB),
+# its MFMA shapes and wave64 layouts; there is no other target
+ARCH = 'gfx950'
+
+
+def _fingerprint(defines=(), extra=(), per_source=None) -> str:
+    """The compiler options a build used (written next to the library)."""
+    import json
+    return json.dumps({'arch': ARCH, 'defines': list(defines), 'extra': list(extra),
+                       'per_source': per_source or SOURCE_FLAGS}, sort_keys=True)
 
 
 def _stale() -> bool:
     if not os.path.isfile(OUT):
         return True
+    # a library built with other options (an A/B variant written over the default path)
+    # is stale even when newer than every source
+    try:
+        with open(OUT + '.flags') as f:
+            if f.read() != _fingerprint():
+                return True
+    except OSError:
+        return True
     t = os.path.getmtime(OUT)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
     deps.append(os.path.join(os.path.dirname(_HERE), 'include', 'siamese_hip.h'))
+    deps.append(os.path.abspath(__file__))
     return any(os.path.isfile(d) and os.path.getmtime(d) > t for d in deps)
 
 
@@ -42,8 +60,14 @@ def build_hip(force: bool = False, verbose: bool = False, out: str = None, defin
             # packed f32 VALU (SLP) blocks DPP fusion and stalls beside MFMA
             '-fno-slp-vectorize',
             '-Wall', '-Wno-unused-function', '-Wno-unused-variable']
+    # A/B options (defines, SG_EXTRA_FLAGS, SG_FLAGS_<SRC>) apply to variants built to an
+    # explicit `out` only: the production library at OUT is always the default build
+    variant = out is not None
+    extra = os.environ.get('SG_EXTRA_FLAGS', '').split() if variant else []
+    defines = tuple(defines) if variant else ()
     base += ['-D' + d for d in defines]
-    base += os.environ.get('SG_EXTRA_FLAGS', '').split()   # A/B of compiler options
+    base += extra
+    per_source = {}
     import tempfile
     with tempfile.TemporaryDirectory(prefix='sg_build_') as tmp:
         procs, objs = [], []
@@ -52,8 +76,10 @@ def build_hip(force: bool = False, verbose: bool = False, out: str = None, defin
             # A/B of one source's options: SG_FLAGS_SG_FAST="..." replaces sg_fast.hip's
             flags = SOURCE_FLAGS.get(src, [])
             env_key = 'SG_FLAGS_' + src.split('.')[0].upper()
-            if env_key in os.environ:
+            if variant and env_key in os.environ:
                 flags = os.environ[env_key].split()
+            if flags:
+                per_source[src] = flags
             cmd = base + flags + ['-c', os.path.join(CSRC, src), '-o', obj]
             if verbose:
                 print(' '.join(cmd))
@@ -77,6 +103,8 @@ def build_hip(force: bool = False, verbose: bool = False, out: str = None, defin
             sys.stderr.write(r.stdout + r.stderr)
             raise RuntimeError('hipcc failed linking libsiamese_hip.so')
     os.replace(dst + '.tmp', dst)
+    with open(dst + '.flags', 'w') as f:
+        f.write(_fingerprint(defines, extra, per_source))
     return dst
 
 

@@ -1206,6 +1206,11 @@ __global__ void __launch_bounds__(256) web_wgrad_kernel_b3(const float *__restri
   __shared__ int act[1024];
   __shared__ int wcnt[4];
   __shared__ float gvh[2][TB];
+  // ≈66.6 KB of static LDS: beyond the 64 KiB of earlier CDNA parts, within gfx950's
+  // 160 KB per CU (the library is built for gfx950 only, build.py)
+  static_assert(2 * 3 * B3PART * sizeof(uint16_t) + 1024 * sizeof(int) + 4 * sizeof(int) +
+                    2 * TB * sizeof(float) <= 160 * 1024,
+                "web_wgrad_kernel_b3 exceeds the gfx950 LDS");
   const int nbt = Dp / TB;
   const int a0 = (blockIdx.x / nbt) * TB, b0 = (blockIdx.x % nbt) * TB;
   const int k = blockIdx.y, s = blockIdx.z;

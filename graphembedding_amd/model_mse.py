@@ -62,6 +62,15 @@ def glorot_flat(layers: List[dict], d_in: int, seed: int = 0) -> np.ndarray:
     return np.concatenate([p.ravel() for p in parts]).astype(np.float32)
 
 
+def splitmix64(x: int) -> int:
+    """Steele et al.'s splitmix64 finaliser (a bijection of 64-bit integers)."""
+    m = 0xFFFFFFFFFFFFFFFF
+    x = (int(x) + 0x9E3779B97F4A7C15) & m
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & m
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & m
+    return x ^ (x >> 31)
+
+
 @dataclass
 class Batch:
     """A packed batch resident on the device (what get_feed_dict returns)."""
@@ -415,14 +424,17 @@ class SiameseGCNTNMSE(object):
 
     # validation draws its dropout masks from a stream of its own: the reference's val
     # sess.run (train.py:19-21) samples independently of the train steps
-    VAL_SEED_STREAM = 1 << 62
+    VAL_SEED_STREAM = 0x5641_4C5F_5354_524D   # 'VAL_STRM'
 
     def val_seed(self, seed=None):
-        """An explicit seed is used as given; the default is the step's seed moved to the
-        validation stream."""
+        """An explicit seed is used as given; the default is the step's seed tagged with
+        the validation stream and put through splitmix64, so both 32-bit halves (and the
+        kernels' 32-bit key lo*C ^ hi) change in every bit position, not by one fixed
+        XOR of the train key (which would make a val pair's masks another pair's train
+        masks)."""
         if seed is not None:
             return int(seed)
-        return (self._seed(None) ^ self.VAL_SEED_STREAM) & 0xFFFFFFFFFFFFFFFF
+        return splitmix64(self._seed(None) ^ self.VAL_SEED_STREAM)
 
     def val_loss(self, batch: Batch, seed=None):
         """sess.run([merged, loss]) on valid_data (train.py:19-21): the loss at the current

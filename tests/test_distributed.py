@@ -115,6 +115,68 @@ def test_rccl_hook_reduces_grad_loss_in_place():
         hook(m2)
 
 
+def _open_worker(rank, world, port, q, case):
+    """open_rccl with injected failures (no GPU: the unique id, the communicator init and
+    the abort are fakes); reports what each rank ended up with and how long it took."""
+    import threading
+    import time
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from graphembedding_amd.rccl import open_rccl
+        aborted = []
+
+        def uid(lib):
+            if case == 'uid_fails' and rank == 0:
+                raise RuntimeError('injected ncclGetUniqueId failure')
+            return b'u' * 128
+
+        def init(lib, raw, r, w):
+            assert raw == b'u' * 128 and w == world
+            if r == 1 and case in ('init_fails_peer_hangs', 'init_fails_peer_ok'):
+                raise RuntimeError('injected ncclCommInitRank failure')
+            if case == 'init_fails_peer_hangs':
+                threading.Event().wait(30)   # a peer stuck in init, waiting for rank 1
+            return 'comm{}'.format(r)
+
+        t0 = time.time()
+        comm, why = open_rccl(rank, world, timeout_s=3.0, _uid=uid, _init=init,
+                              _abort=lambda lib, c: aborted.append(c))
+        dist.barrier()   # both ranks still talk over the process group afterwards
+        q.put((rank, None if comm is None else comm.comm, why, aborted, time.time() - t0))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('case', ['ok', 'uid_fails', 'init_fails_peer_ok',
+                                  'init_fails_peer_hangs'])
+def test_open_rccl_ranks_agree(case):
+    """bench.py's collective choice is the same on every rank: open_rccl returns a
+    communicator on both ranks or on neither, whichever rank fails (rank 0's unique id,
+    one rank's init while the peer's succeeds, one rank's init while the peer's stalls),
+    and no rank waits past the init timeout."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_open_worker, args=(r, 2, port, q, case)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    comms = [o[1] for o in out]
+    if case == 'ok':
+        assert comms == ['comm0', 'comm1']
+        assert all(o[2] is None for o in out)
+        return
+    assert comms == [None, None], out
+    assert all(o[2] for o in out), out   # every rank says why it falls back
+    assert all(o[4] < 20.0 for o in out), out
+    if case == 'init_fails_peer_ok':   # rank 0 held a communicator its peer gave up on
+        assert out[0][3] == ['comm0'] and out[1][3] == []
+
+
 def test_rccl_binding_loads():
     """graphembedding_amd.rccl binds torch's own librccl.so (the symbols the direct
     collective uses) and draws a unique id without touching a GPU."""

@@ -2,7 +2,10 @@
 as bench.py runs it for N > 1), at world size 1 so it fits a one-GPU box: the in-place
 SUM all-reduce of model.grad_loss goes through RCCL on device memory and must leave
 the step bitwise unchanged.  World sizes > 1 are covered by the gloo test in
-test_distributed.py (shards + all-reduce == the single-process step)."""
+test_distributed.py (shards + all-reduce == the single-process step), and on a node
+with two or more GPUs by the two-rank direct-RCCL sum at the end of this file."""
+import os
+
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -77,3 +80,54 @@ def test_rccl_direct_world1_hook_keeps_step_bitwise(gpu):
     a, b = models
     assert torch.equal(a.grad_loss, b.grad_loss)
     assert torch.equal(a.params, b.params)
+
+
+def _two_rank_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.cuda.set_device(rank)
+    dev = torch.device('cuda', rank)
+    dist.init_process_group('nccl', rank=rank, world_size=world, device_id=dev)
+    try:
+        from graphembedding_amd.rccl import open_rccl
+        comm, why = open_rccl(rank, world)
+        assert comm is not None, why
+        n = 2727   # an odd count: a wrong count or datatype enum would show
+        g = torch.Generator().manual_seed(100 + rank)
+        x = torch.randn(n, generator=g, dtype=torch.float32).to(dev)
+        a, b = x.clone(), x.clone()
+        comm.all_reduce_sum_(a)
+        dist.all_reduce(b, op=dist.ReduceOp.SUM)
+        torch.cuda.synchronize()
+        expect = sum(torch.randn(n, generator=torch.Generator().manual_seed(100 + r),
+                                 dtype=torch.float32).double() for r in range(world))
+        q.put((rank, float((a.cpu().double() - expect).abs().max()),
+               bool(torch.equal(a, b))))
+        comm.destroy()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.skipif(__import__('torch').cuda.device_count() < 2,
+                    reason='needs two GPUs (the round-end 8-GPU node); a one-GPU box skips it')
+def test_rccl_direct_two_ranks_sum(gpu):
+    """Two ranks, one GPU each: RcclComm.all_reduce_sum_ (opened by open_rccl) gives the
+    exact sum of distinct per-rank buffers and equals torch.distributed's all-reduce."""
+    import socket
+    import torch.multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    procs = [ctx.Process(target=_two_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, err, same in out:
+        assert err <= 1e-5, (rank, err)
+        assert same, rank

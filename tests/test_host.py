@@ -203,13 +203,29 @@ def test_graph_larger_than_padding_dim_is_refused():
 
 
 def test_validation_seed_stream_is_distinct():
-    """val_loss draws dropout masks independently of the train steps (ADVICE r1): its
-    default seed is never a train-step seed."""
+    """val_loss draws dropout masks independently of the train steps (ADVICE r1, r2): its
+    default seed is never a train-step seed, and at the level the kernels use (the
+    32-bit key and the dropout masks) the validation stream is not a fixed XOR of the
+    train stream."""
     from graphembedding_amd.model_mse import SiameseGCNTNMSE
     prob = small_problem(n_graphs=4, n_pairs=3, seed=3)
     model = SiameseGCNTNMSE(prob.d_in, prob.flags, device='cpu', params=prob.params)
     train = {model._seed(None) + k for k in range(-50, 50)}
+    train_keys = {O.seed_key(s) for s in train}
+    diffs = set()
     for step in range(20):
         model.step_count = step
         assert model.val_seed() not in train
         assert model.val_seed(123) == 123
+        kv, kt = O.seed_key(model.val_seed()), O.seed_key(model._seed(None))
+        assert kv not in train_keys
+        diffs.add(kv ^ kt)
+        assert bin(kv ^ kt).count('1') >= 6, hex(kv ^ kt)
+        # masks: a val pair's masks are neither its own train masks nor those of the
+        # pair the old one-bit XOR mapped it to
+        for p in range(8):
+            mv = O.dropout_mask(model.val_seed(), p, 0, 1, 320, 0.9)
+            for q in (p, p ^ (1 << 30)):
+                assert not np.array_equal(mv, O.dropout_mask(model._seed(None), q, 0, 1, 320,
+                                                             0.9)), (step, p, q)
+    assert len(diffs) == 20   # no fixed key offset between the streams
