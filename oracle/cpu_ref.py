@@ -28,15 +28,18 @@ def lib():
                                   vp, ctypes.c_uint64, ctypes.c_float, ctypes.c_float,
                                   ctypes.c_float, vp, vp, vp, ctypes.c_int]
         L.sgc_fwd_bwd.restype = ctypes.c_int
+        L.sgc_fwd_bwd_f64acc.argtypes = L.sgc_fwd_bwd.argtypes
+        L.sgc_fwd_bwd_f64acc.restype = ctypes.c_int
         _lib = L
     return _lib
 
 
 def fwd_bwd_records(words: np.ndarray, n_max: int, d_in: int, params: np.ndarray, seed: int,
                     keep: float, yeta: float, ybar: float, pair_offset: int = 0,
-                    threads: int = 1):
+                    threads: int = 1, f64_acc: bool = False):
     """Default-stack fwd+bwd over host records (uint32 [P][W]).
-    Returns (s [P], grad_mse [n_params], loss ½Σ(ŷ-ȳ)²)."""
+    Returns (s [P], grad_mse [n_params], loss ½Σ(ŷ-ȳ)²).  f64_acc: the same float32
+    per-pair arithmetic with the gradient summed in double (the full-batch checker)."""
     L = lib()
     words = np.ascontiguousarray(words, dtype=np.uint32)
     P = words.shape[0]
@@ -46,13 +49,23 @@ def fwd_bwd_records(words: np.ndarray, n_max: int, d_in: int, params: np.ndarray
     s = np.zeros(P, np.float32)
     g = np.zeros(npar, np.float32)
     loss = ctypes.c_double(0.0)
-    rc = L.sgc_fwd_bwd(words.ctypes.data, P, int(pair_offset), int(n_max), int(d_in),
+    fn = L.sgc_fwd_bwd_f64acc if f64_acc else L.sgc_fwd_bwd
+    rc = fn(words.ctypes.data, P, int(pair_offset), int(n_max), int(d_in),
                        params.ctypes.data, int(seed) & 0xFFFFFFFFFFFFFFFF, float(keep),
                        float(yeta), float(ybar), s.ctypes.data, g.ctypes.data,
                        ctypes.addressof(loss), int(threads))
     if rc != 0:
         raise RuntimeError('sgc_fwd_bwd failed')
     return s, g, float(loss.value)
+
+
+def adam_step(params: np.ndarray, grad_mse: np.ndarray, st, flags) -> np.ndarray:
+    """The step's ApplyAdam (models.py:28-36, TF form) with weight decay on every variable
+    (models.py:67-74, quirk A10), as the timed GPU step runs it after fwd+bwd."""
+    from oracle import siamese_oracle as O
+    g = grad_mse.astype(np.float64) + flags.weight_decay * params.astype(np.float64)
+    return O.adam_tf_step(params.astype(np.float64), g, st,
+                          lr=flags.learning_rate).astype(np.float32)
 
 
 def default_threads() -> int:
@@ -89,11 +102,15 @@ def time_allpairs_sample(gs, labels, flags, n_sample: int = 0, target_s: float =
         return cache[n]
 
     def run(n, reps=1):
+        from oracle import siamese_oracle as O
         w = words_for(n)
+        p = params.copy()
+        st = O.adam_init(p.size)
         t0 = time.perf_counter()
-        for r in range(reps):
-            fwd_bwd_records(w, gs.n_max, gs.d_in, params, 1 + r, 1.0 - flags.dropout, flags.yeta,
-                            ybar, threads=threads)
+        for r in range(reps):   # one training step: fwd+bwd, then Adam, like the GPU step
+            _, g, _ = fwd_bwd_records(w, gs.n_max, gs.d_in, p, 1 + r, 1.0 - flags.dropout,
+                                      flags.yeta, ybar, threads=threads)
+            p = adam_step(p, g, st, flags)
         return time.perf_counter() - t0
 
     reps = 1
@@ -111,8 +128,9 @@ def time_allpairs_sample(gs, labels, flags, n_sample: int = 0, target_s: float =
             else 'first {} pairs of the all-pairs stream'.format(n_sample))
     return {'value': n_sample * reps / dt, 'unit': 'graph-pairs/s', 'cores': threads,
             'kind': 'port',
-            'sample': '{}, fwd+bwd (loss + grads, no Adam), C restatement oracle/siamese_cpu.c, '
-                      'fp32, OpenMP {} threads, {:.1f} s'.format(what, threads, dt)}
+            'sample': '{}, one training step each (fwd+bwd: loss + grads, then TF Adam with '
+                      'weight decay), C restatement oracle/siamese_cpu.c, fp32, OpenMP {} '
+                      'threads, {:.1f} s'.format(what, threads, dt)}
 
 
 def time_web_sample(gs, labels, flags, n_sample: int = 32, target_s: float = 12.0,
@@ -134,11 +152,14 @@ def time_web_sample(gs, labels, flags, n_sample: int = 32, target_s: float = 12.
     uniq, inv = np.unique(pairs.reshape(-1), return_inverse=True)
     store = GraphStore([gs.mgs[i] for i in uniq], gs.n_max, gs.d_in)
     words = store.pack_host(inv.reshape(-1, 2), labels.reshape(-1)[p])
+    from oracle import siamese_oracle as O
+    st = O.adam_init(params.size)
     t0 = time.perf_counter()
     reps = 0
     while True:
-        fwd_bwd_records(words, gs.n_max, gs.d_in, params, 1 + reps, 1.0 - flags.dropout,
-                        flags.yeta, ybar, threads=threads)
+        _, g, _ = fwd_bwd_records(words, gs.n_max, gs.d_in, params, 1 + reps,
+                                  1.0 - flags.dropout, flags.yeta, ybar, threads=threads)
+        params = adam_step(params, g, st, flags)
         reps += 1
         dt = time.perf_counter() - t0
         if dt >= target_s:
@@ -146,6 +167,6 @@ def time_web_sample(gs, labels, flags, n_sample: int = 32, target_s: float = 12.
     return {'value': n_sample * reps / dt, 'unit': 'graph-pairs/s', 'cores': threads,
             'kind': 'port',
             'sample': '{} x {} random pairs of the all-pairs stream (seed {}), fwd+bwd (loss + '
-                      'grads, no Adam), C restatement oracle/siamese_cpu.c on dense capacity-{} '
+                      'grads) + TF Adam per pass, C restatement oracle/siamese_cpu.c on dense capacity-{} '
                       'records, fp32, OpenMP {} threads, {:.1f} s'.format(
                           reps, n_sample, seed, gs.n_max, threads, dt)}

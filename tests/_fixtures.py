@@ -122,3 +122,31 @@ def run_oracle_step(prob: Problem, seed: int, adam: bool = True):
         st = O.adam_init(flat.size)
         res.new_params = O.adam_tf_step(flat, res.grad, st, lr=prob.flags.learning_rate)
     return res
+
+
+def check_grad_per_var(g_gpu, g_ref, layers, d_in, tol=1e-4, what=''):
+    """Per-variable gradient check: every variable of the flat gradient (the
+    reference's variable order, model_mse.param_shapes) must match within `tol` x the
+    largest |component| of that variable's own reference gradient — a few-percent error
+    in a small-magnitude tensor (NTN bias, U, b1) cannot hide behind the largest one.
+    The floor (1e-7 x the global max) only keeps an all-zero variable from dividing by
+    zero.  Returns {variable: relative error} for reporting."""
+    from graphembedding_amd.model_mse import param_shapes
+    g_gpu = np.asarray(g_gpu, np.float64).reshape(-1)
+    g_ref = np.asarray(g_ref, np.float64).reshape(-1)
+    assert g_gpu.shape == g_ref.shape, (g_gpu.shape, g_ref.shape)
+    floor = 1e-7 * max(float(np.abs(g_ref).max()), 1e-30)
+    off, rel, bad = 0, {}, []
+    for li, name, shape in param_shapes(layers, d_in):
+        n = int(np.prod(shape))
+        a, b = g_gpu[off:off + n], g_ref[off:off + n]
+        scale = max(float(np.abs(b).max()), floor)
+        r = float(np.abs(a - b).max()) / scale
+        key = '{}.{}'.format(li, name)
+        rel[key] = r
+        if not r <= tol:
+            bad.append((key, r, scale))
+        off += n
+    assert off == g_ref.size
+    assert not bad, '{} per-variable gradient errors above {}: {}'.format(what, tol, bad)
+    return rel

@@ -9,7 +9,8 @@ Pinned here (reference modules imported read-only, PYTHONDONTWRITEBYTECODE):
   model/Siamese/samplers.py   RandomSampler / DistributionSampler pair streams
   src/similarity.py           GaussianKernel / IdentityKernel, create_sim_kernel
   src/metrics.py              precision_at_ks, mean_reciprocal_rank, mean_squared_error
-  src/utils.py                sorted_nicely
+  src/utils.py                sorted_nicely, save (F6: the label-store pickle)
+  src/data.py                 AIDS700nefData / AIDS80nefData gexf loaders (F6)
 Not importable here: TF (absent), src/distance.py and src/results.py (need bs4
 via nx_to_gxl.py) — their logic is restated and tested against these fixtures
 where it feeds them.
@@ -144,5 +145,122 @@ def main():
     print('golden fixtures written to', HERE)
 
 
+def f6_gexf_tree(root):
+    """A small AIDS700nef-shaped gexf tree (data/AIDS700nef/{train,test}/<gid>.gexf):
+    84 train + 14 test connected graphs of 3-8 nodes, gids deliberately not in
+    lexicographic order (sorted_nicely matters), node ids in a shuffled file order (the
+    node order of read_gexf is the file order, quirk A8), and a 'valence' edge attribute
+    on some edges (the nef loaders drop it, data.py:80-83,91-93)."""
+    rng = np.random.default_rng(606)
+    gid = 0
+    for split, count in (('train', 84), ('test', 14)):
+        d = os.path.join(root, 'AIDS700nef', split)
+        os.makedirs(d, exist_ok=True)
+        for k in range(count):
+            gid += int(rng.integers(1, 40))
+            n = int(rng.integers(3, 9))
+            g0 = synthetic_graph(rng, n, gid, 29, p_extra=0.2)
+            order = [str(v) for v in rng.permutation(n)]
+            g = nx.Graph()
+            for v in order:
+                g.add_node(v, type=g0.nodes[v]['type'], label=v)
+            for u, v in g0.edges():
+                if rng.random() < 0.5:
+                    g.add_edge(u, v, valence=int(rng.integers(1, 3)))
+                else:
+                    g.add_edge(u, v)
+            nx.write_gexf(g, os.path.join(d, '{}.gexf'.format(gid)))
+
+
+def f6_loaders():
+    """F6 (rows f2/f3): the reference's own on-disk loaders and label store.
+
+    f2: gexf files read by the reference's AIDS700nefData / AIDS80nefData
+        (src/data.py:62-132, nx.read_gexf + sorted_nicely + connectivity check + valence
+        removal; AIDS80nef = Random(123).shuffle then the first 70 / 10), with
+        get_data_path / get_save_path pointed at a temporary tree.
+    f3: a gid-pair distance map (OrderedDict{(gid1, gid2): int},
+        model/Siamese/dist_calculator.py:8-20) written by the reference's utils.save
+        (src/utils.py:203-234), and GED / time result matrices saved under the names
+        src/exp.py:263-266 writes (result/<ds>/ged/ged_ged_mat_<ds>_<model>_<ts>_...npy),
+        which src/results.py:182-192 globs."""
+    import shutil
+    import tempfile
+    from collections import OrderedDict
+    import data as ref_data  # noqa: E402  (reference)
+    fx = os.path.join(HERE, 'f6')
+    if os.path.isdir(fx):
+        shutil.rmtree(fx)
+    data_root = os.path.join(fx, 'data')
+    f6_gexf_tree(data_root)
+    out = {}
+    with tempfile.TemporaryDirectory() as save_dir:
+        # the reference module bound these names at import (from utils import ...)
+        ref_data.get_data_path = lambda: data_root
+        ref_data.get_save_path = lambda: save_dir
+        for cls in ('AIDS700nefData', 'AIDS80nefData'):
+            for train in (True, False):
+                d = getattr(ref_data, cls)(train)
+                key = '{}_{}'.format(cls, 'train' if train else 'test')
+                out[key] = [{'gid': g.graph['gid'],
+                             'nodes': [[v, g.nodes[v].get('type')] for v in g.nodes()],
+                             'edges': sorted([sorted([u, v]) + [sorted(a.keys())]
+                                              for u, v, a in g.edges(data=True)])}
+                            for g in d.graphs]
+    # f3: the label store
+    tr = [g['gid'] for g in out['AIDS80nefData_train']]
+    te = [g['gid'] for g in out['AIDS80nefData_test']]
+    sizes = {g['gid']: len(g['nodes']) for k in ('AIDS80nefData_train', 'AIDS80nefData_test')
+             for g in out[k]}
+    rng = np.random.default_rng(808)
+    dmap = OrderedDict()
+    entries = []
+    for a in te:
+        for b in tr[:20]:
+            d = int(rng.integers(0, 9))
+            rev = bool(rng.random() < 0.5)
+            if not rev:
+                dmap[(a, b)] = d
+            else:                       # stored reversed: found through the reverse key
+                dmap[(b, a)] = d
+            entries.append([a, b, d, rev])
+    # a cached reverse distance of 0 is treated as a miss (dist_calculator.py:33-37, A15)
+    zero_pair = [te[0], tr[25]]
+    dmap[(tr[25], te[0])] = 0
+    save_dir = os.path.join(fx, 'save')
+    os.makedirs(save_dir, exist_ok=True)
+    ref_utils.save(os.path.join(save_dir, 'aids80nef_ged_astar_gidpair_dist_map'), dmap)
+    m, n = len(te), len(tr)
+    ged_mat = np.zeros((m, n))                       # exp.py:219-220
+    time_mat = np.zeros((m, n))
+    for i in range(m):
+        for j in range(n):
+            ged_mat[i][j] = int(rng.integers(0, 9))
+            time_mat[i][j] = float(np.round(rng.random() * 3, 2))
+    rdir = os.path.join(fx, 'result', 'aids80nef')
+    os.makedirs(os.path.join(rdir, 'ged'), exist_ok=True)
+    os.makedirs(os.path.join(rdir, 'time'), exist_ok=True)
+    stamp = '2018-06-01T10:00:00_host_8cpus'
+    np.save(os.path.join(rdir, 'ged', 'ged_ged_mat_aids80nef_astar_{}'.format(stamp)), ged_mat)
+    np.save(os.path.join(rdir, 'time', 'ged_time_mat_aids80nef_astar_{}'.format(stamp)),
+            time_mat)
+    # normalized_dist (distance.py:59-60) of every (test i, train j) result entry
+    norm = np.array([[2.0 * ged_mat[i][j] / (sizes[te[i]] + sizes[tr[j]]) for j in range(n)]
+                     for i in range(m)])
+    out['dist_map_entries'] = entries
+    out['dist_map_reverse_zero_pair'] = zero_pair
+    out['dist_map_len'] = len(dmap)
+    out['ged_mat'] = ged_mat.tolist()
+    out['time_mat'] = time_mat.tolist()
+    out['ged_norm_mat'] = norm.tolist()
+    with open(os.path.join(HERE, 'f6_loaders.json'), 'w') as f:
+        json.dump(out, f)
+    print('F6 fixtures written to', fx)
+
+
 if __name__ == '__main__':
-    main()
+    if '--only-f6' in sys.argv:
+        f6_loaders()
+    else:
+        main()
+        f6_loaders()

@@ -126,3 +126,86 @@ def test_f4_metrics_and_result_ranking():
 def test_f5_sorted_nicely():
     f5 = _load('f5_utils.json')
     assert sorted_nicely(f5['in']) == f5['sorted_nicely']
+
+
+# ---- F6: the reference's on-disk loaders and label store ----
+F6 = os.path.join(G, 'f6')
+
+
+def _graph_record(g):
+    return {'gid': g.graph['gid'],
+            'nodes': [[v, g.nodes[v].get('type')] for v in g.nodes()],
+            'edges': sorted([sorted([u, v]) + [sorted(a.keys())]
+                             for u, v, a in g.edges(data=True)])}
+
+
+def test_f6_gexf_loaders_match_reference(monkeypatch, tmp_path):
+    """AIDS700nefData / AIDS80nefData over the committed gexf tree give exactly the graphs
+    the reference's loaders gave (src/data.py:62-132): gids in sorted_nicely file order,
+    read_gexf node order (A8) and types, valence removed, and AIDS80nef's
+    Random(123).shuffle + first 70 / 10.  Through load_data, as utils.py:15-35."""
+    from graphembedding_amd.utils import load_data
+    monkeypatch.setenv('SG_DATA_PATH', os.path.join(F6, 'data'))
+    monkeypatch.setenv('SG_SAVE_PATH', str(tmp_path))
+    f6 = _load('f6_loaders.json')
+    for ds, cls in (('aids700nef', 'AIDS700nefData'), ('aids80nef', 'AIDS80nefData')):
+        for train in (True, False):
+            key = '{}_{}'.format(cls, 'train' if train else 'test')
+            got = [_graph_record(g) for g in load_data(ds, train).graphs]
+            assert got == f6[key], key
+    # the pickle cache (data.py:10-21): a second load comes from save/ and is identical
+    assert os.path.isfile(os.path.join(str(tmp_path), 'AIDS80nefData_train.pickle'))
+    again = [_graph_record(g) for g in load_data('aids80nef', True).graphs]
+    assert again == f6['AIDS80nefData_train']
+
+
+def test_f6_gid_pair_map_written_by_reference(monkeypatch, tmp_path):
+    """The gid-pair distance map pickle written by the reference's utils.save is read by
+    DistCalculator (restricted unpickler): forward and reverse keys, normalized_dist, and
+    a cached reverse 0 treated as a miss (dist_calculator.py:26-44, quirk A15)."""
+    from graphembedding_amd.dist_calculator import DistCalculator
+    from graphembedding_amd.utils import load_data, safe_load
+    monkeypatch.setenv('SG_DATA_PATH', os.path.join(F6, 'data'))
+    monkeypatch.setenv('SG_SAVE_PATH', os.path.join(F6, 'save'))
+    f6 = _load('f6_loaders.json')
+    raw = safe_load(os.path.join(F6, 'save', 'aids80nef_ged_astar_gidpair_dist_map'))
+    assert type(raw).__name__ == 'OrderedDict' and len(raw) == f6['dist_map_len']
+    monkeypatch.setenv('SG_SAVE_PATH', str(tmp_path))
+    by_gid = {g.graph['gid']: g for tv in (True, False)
+              for g in load_data('aids80nef', tv).graphs}
+    monkeypatch.setenv('SG_SAVE_PATH', os.path.join(F6, 'save'))
+    dc = DistCalculator('aids80nef', 'ged', 'astar')
+    assert len(dc.gidpair_dist_map) == f6['dist_map_len']
+    n_rev_zero = 0
+    for a, b, d, rev in f6['dist_map_entries']:
+        g1, g2 = by_gid[a], by_gid[b]
+        if rev and d == 0:   # stored reversed as 0: a miss, like the reference (A15)
+            with pytest.raises(RuntimeError, match='GED ground truth'):
+                dc.calculate_dist(g1, g2)
+            n_rev_zero += 1
+            continue
+        got, nd = dc.calculate_dist(g1, g2)
+        assert got == d
+        assert nd == 2 * d / (g1.number_of_nodes() + g2.number_of_nodes())
+    assert n_rev_zero > 0
+    a, b = f6['dist_map_reverse_zero_pair']
+    with pytest.raises(RuntimeError, match='GED ground truth'):
+        dc.calculate_dist(by_gid[a], by_gid[b])   # reverse 0 -> miss -> the GED solver
+
+
+def test_f6_result_matrices_under_reference_names(monkeypatch, tmp_path):
+    """GED / time matrices saved under src/exp.py:263-266's names are found by the
+    results.py:182-192 glob; the normalized matrix uses the test x train graphs of the
+    dataset (results.py:129-144)."""
+    from graphembedding_amd.results import PairwiseGEDModelResult, load_result
+    monkeypatch.setenv('SG_DATA_PATH', os.path.join(F6, 'data'))
+    monkeypatch.setenv('SG_SAVE_PATH', str(tmp_path))
+    monkeypatch.setenv('SG_RESULT_PATH', os.path.join(F6, 'result'))
+    f6 = _load('f6_loaders.json')
+    r = PairwiseGEDModelResult('aids80nef', 'astar')
+    assert np.array_equal(r.dist_mat(False), np.array(f6['ged_mat']))
+    assert np.array_equal(r.dist_mat(True), np.array(f6['ged_norm_mat']))
+    assert np.array_equal(r.time_mat(), np.array(f6['time_mat']))
+    assert r.m_n() == (10, 70)
+    r2 = load_result('aids80nef', 'astar')
+    assert np.array_equal(r2.dist_mat(True), r.dist_mat(True))

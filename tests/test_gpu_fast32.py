@@ -4,7 +4,7 @@ oracle and against the generic kernel.  Tolerance 1e-4 (north_star)."""
 import numpy as np
 import pytest
 
-from _fixtures import run_oracle_step, small_problem
+from _fixtures import check_grad_per_var, run_oracle_step, small_problem
 
 pytestmark = pytest.mark.gpu
 
@@ -21,10 +21,9 @@ CASES = {
 }
 
 
-def _check_grad(g_gpu, g_ref, tol=TOL):
-    scale = max(1.0, float(np.abs(g_ref).max()))
-    err = float(np.abs(g_gpu - g_ref).max())
-    assert err <= tol * scale, 'max |grad err| {} (scale {})'.format(err, scale)
+def _check_grad(g_gpu, g_ref, prob, tol=TOL):
+    """Per variable, each against its own largest reference component (_fixtures)."""
+    check_grad_per_var(g_gpu, g_ref, prob.layers, prob.d_in, tol)
 
 
 @pytest.mark.parametrize('name', list(CASES))
@@ -39,7 +38,7 @@ def test_fast32_matches_oracle(gpu, name):
     s = model.pred_sim_without_act(batch, seed=seed).cpu().numpy()
     np.testing.assert_allclose(s, ref.s, rtol=TOL, atol=TOL)
     model.fwd_bwd(batch, seed=seed)
-    _check_grad(model.grad.cpu().numpy(), ref.grad_mse)
+    _check_grad(model.grad.cpu().numpy(), ref.grad_mse, prob)
     loss_mse = float(model.loss_buf[0].item())
     assert abs(loss_mse - ref.loss_mse) <= TOL * max(1.0, abs(ref.loss_mse))
     model.apply_adam()
@@ -65,13 +64,13 @@ def test_fast32_matches_generic_and_is_reproducible(gpu, monkeypatch):
     model.balance(batch)
     assert np.array_equal(model.pred_sim_without_act(batch, seed=seed).cpu().numpy(), s32)
     model.fwd_bwd(batch, seed=seed)
-    _check_grad(model.grad.cpu().numpy(), g32.cpu().numpy(), tol=1e-5)
+    _check_grad(model.grad.cpu().numpy(), g32.cpu().numpy(), prob, tol=1e-5)
     batch.order = None
     monkeypatch.setenv('SG_DISABLE_FAST', '1')
     s_gen = model.pred_sim_without_act(batch, seed=seed).cpu().numpy()
     model.fwd_bwd(batch, seed=seed)
     np.testing.assert_allclose(s32, s_gen, rtol=1e-5, atol=1e-5)
-    _check_grad(g32.cpu().numpy(), model.grad.cpu().numpy(), tol=2e-5)
+    _check_grad(g32.cpu().numpy(), model.grad.cpu().numpy(), prob, tol=2e-5)
     assert abs(l32 - float(model.loss_buf[0].item())) <= 1e-5 * max(1.0, abs(l32))
 
 

@@ -1,0 +1,90 @@
+"""Full-batch parity at the headline configs: EVERY score and the
+whole gradient of the bench's step, against the oracle's C restatement
+(oracle/siamese_cpu.c, float32 per-pair arithmetic like TF-CPU, gradients summed in
+double) on the same records, dropout on (shared counter RNG).
+
+- C2: AIDS700nef all-pairs, 490,000 pairs, f32 records, class order (as bench.py runs
+  it), plus an 8-rank shard whose global pair offset keys the dropout masks.
+- C3: the same step with bf16 Â records; the checker runs on records whose Â is the
+  bf16 value widened back to f32 (what the kernels compute with).
+Tolerances: scores 1e-4 (north_star); gradient 1e-4 of each variable's own largest
+component (per variable: W0, b0, W1, b1, Wd, bd, W, V, U, b); loss 1e-4 relative.
+Reference math: layers.py:91-310, model_mse.py:145-151, models.py:67-73."""
+import numpy as np
+import pytest
+
+from _fixtures import check_grad_per_var
+from oracle import cpu_ref
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def _checker(model, gs, shard, seed, dtype):
+    """The C restatement over the shard's records (host-packed from the same store)."""
+    from graphembedding_amd.packer import GraphStore, bf16_round
+    G = len(gs.graphs)
+    p = np.arange(shard.start, shard.end, dtype=np.int64)
+    pairs = np.stack([p // G, p % G], axis=1)
+    store = gs.store
+    if dtype == 'bf16':
+        store = GraphStore(gs.mgs, gs.n_max, gs.d_in)
+        store.adj = bf16_round(store.adj.astype(np.float32))
+    lab = shard.labels.cpu().numpy()
+    words = store.pack_host(pairs, lab, dtype='f32')
+    ybar = float(shard.y_stats[0].item())
+    params = model.params.cpu().numpy()
+    s, g, loss = cpu_ref.fwd_bwd_records(words, gs.n_max, gs.d_in, params, seed,
+                                         1.0 - model.flags.dropout, model.flags.yeta, ybar,
+                                         pair_offset=shard.start,
+                                         threads=cpu_ref.default_threads(), f64_acc=True)
+    return s, g, loss
+
+
+def _run(gpu, dtype, rank=0, world=1):
+    import torch
+    from graphembedding_amd.allpairs import AllPairsShard, load_graph_set
+    from graphembedding_amd.config import Flags
+    from graphembedding_amd.model_mse import SiameseGCNTNMSE
+    f = Flags(dropout=0.1, record_dtype=dtype)
+    gs = load_graph_set('syn_aids700nef', n_max=10)
+    labels = gs.label_matrix(f.yeta)
+    model = SiameseGCNTNMSE(gs.d_in, f, device=gpu, n_max=gs.n_max)
+    assert model.kernel_path == 1 and model.record_dtype == dtype
+    shard = AllPairsShard(gs, labels, rank, world, device=gpu, dtype=dtype)
+    batch = shard.batch(model, balance=True)     # bench.py's class order
+    seed = 20251
+    s_out = torch.full((batch.n_pairs,), float('nan'), dtype=torch.float32, device=gpu)
+    model.fwd_bwd(batch, seed=seed, s_out=s_out, add_label_term=(rank == 0))
+    g_gpu = model.grad.cpu().numpy().astype(np.float64)
+    loss_gpu = float(model.loss_buf[0].item())
+    s_fwd = model.pred_sim_without_act(batch, seed=seed).cpu().numpy()
+    s_ref, g_ref, loss_ref = _checker(model, gs, shard, seed, dtype)
+    # every score of the training step and of the forward-only (eval) path
+    s_bwd = s_out.cpu().numpy()
+    assert not np.isnan(s_bwd).any()
+    np.testing.assert_allclose(s_bwd, s_ref, rtol=TOL, atol=TOL)
+    np.testing.assert_allclose(s_fwd, s_ref, rtol=TOL, atol=TOL)
+    rel = check_grad_per_var(g_gpu, g_ref, model.layers, model.input_dim, TOL,
+                             what='{} rank {}/{}'.format(dtype, rank, world))
+    # loss_mse = ½Σ(ŷ-ȳ)² (+ the label term ½Σ(y-ȳ)² on rank 0), model_mse.py:145-151
+    label_term = float(shard.y_stats[1].item()) if rank == 0 else 0.0
+    assert abs(loss_gpu - (loss_ref + label_term)) <= TOL * max(1.0, abs(loss_ref + label_term))
+    return rel
+
+
+def test_c2_full_step_every_pair_and_gradient(gpu):
+    rel = _run(gpu, 'f32')
+    print('C2 per-variable relative gradient error:', rel)
+
+
+def test_c3_bf16_full_step_every_pair_and_gradient(gpu):
+    rel = _run(gpu, 'bf16')
+    print('C3 per-variable relative gradient error:', rel)
+
+
+def test_c2_rank_shard_every_pair_and_gradient(gpu):
+    """Rank 5 of an 8-GPU step: 61,250 pairs at global offset 306,250 (dropout keys),
+    no label term; the gradient is this rank's share of the all-reduce."""
+    _run(gpu, 'f32', rank=5, world=8)

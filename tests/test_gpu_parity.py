@@ -4,7 +4,7 @@ Tolerance: 1e-4 (north_star: per-pair scores within 1e-4 fp32)."""
 import numpy as np
 import pytest
 
-from _fixtures import AVERAGE_STACK, run_oracle_step, small_problem
+from _fixtures import AVERAGE_STACK, check_grad_per_var, run_oracle_step, small_problem
 from oracle import siamese_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -30,10 +30,9 @@ STACKS = {
 }
 
 
-def _check_grad(g_gpu, g_ref, tol=TOL):
-    scale = max(1.0, float(np.abs(g_ref).max()))
-    err = float(np.abs(g_gpu - g_ref).max())
-    assert err <= tol * scale, 'max |grad err| {} (scale {})'.format(err, scale)
+def _check_grad(g_gpu, g_ref, prob, tol=TOL):
+    """Per variable, each against its own largest reference component (_fixtures)."""
+    check_grad_per_var(g_gpu, g_ref, prob.layers, prob.d_in, tol)
 
 
 @pytest.mark.parametrize('name', list(STACKS))
@@ -45,7 +44,7 @@ def test_forward_and_step_match_oracle(gpu, name):
     ref = run_oracle_step(prob, seed)
     np.testing.assert_allclose(s, ref.s, rtol=TOL, atol=TOL)
     model.fwd_bwd(batch, seed=seed)
-    _check_grad(model.grad.cpu().numpy(), ref.grad_mse)
+    _check_grad(model.grad.cpu().numpy(), ref.grad_mse, prob)
     loss_mse = float(model.loss_buf[0].item())
     assert abs(loss_mse - ref.loss_mse) <= TOL * max(1.0, abs(ref.loss_mse))
     model.apply_adam()
@@ -79,7 +78,7 @@ def test_large_batch_properties(gpu):
     g0 = model.grad.clone()
     model.fwd_bwd(b1, seed=seed, add_label_term=False)
     g_sum = (g0 + model.grad).cpu().numpy()
-    _check_grad(g_sum, g_full.cpu().numpy(), tol=1e-5)
+    _check_grad(g_sum, g_full.cpu().numpy(), prob, tol=1e-5)
 
 
 @pytest.mark.parametrize('dtype', ['f32', 'bf16'])
@@ -137,7 +136,7 @@ def test_nmax30_aids10k_shape(gpu):
     ref = run_oracle_step(prob, 5)
     np.testing.assert_allclose(s, ref.s, rtol=TOL, atol=TOL)
     model.fwd_bwd(batch, seed=5)
-    _check_grad(model.grad.cpu().numpy(), ref.grad_mse)
+    _check_grad(model.grad.cpu().numpy(), ref.grad_mse, prob)
 
 
 @pytest.mark.parametrize('stack', ['default', 'average'])
@@ -159,7 +158,7 @@ def test_fast_path_matches_generic_path(gpu, monkeypatch, stack):
     model.fwd_bwd(batch, seed=seed)
     g_gen = model.grad.cpu().numpy()
     np.testing.assert_allclose(s_fast, s_gen, rtol=1e-5, atol=1e-5)
-    _check_grad(g_fast, g_gen, tol=2e-5)
+    _check_grad(g_fast, g_gen, prob, tol=2e-5)
     assert abs(l_fast - float(model.loss_buf[0].item())) <= 1e-5 * max(1.0, abs(l_fast))
 
 
@@ -192,6 +191,6 @@ def test_fused_path_edge_shapes(gpu, case):
     ref = run_oracle_step(prob, seed)
     np.testing.assert_allclose(s, ref.s, rtol=TOL, atol=TOL)
     model.fwd_bwd(batch, seed=seed)
-    _check_grad(model.grad.cpu().numpy(), ref.grad_mse)
+    _check_grad(model.grad.cpu().numpy(), ref.grad_mse, prob)
     loss_mse = float(model.loss_buf[0].item())
     assert abs(loss_mse - ref.loss_mse) <= TOL * max(1.0, abs(ref.loss_mse))

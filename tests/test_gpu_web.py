@@ -7,7 +7,7 @@ are synthetic and the parity anchor is the oracle, not reference fixtures."""
 import numpy as np
 import pytest
 
-from _fixtures import run_oracle_step, small_problem
+from _fixtures import check_grad_per_var, run_oracle_step, small_problem
 
 pytestmark = pytest.mark.gpu
 
@@ -32,10 +32,9 @@ def _problem(name, seed=31):
                          flags_overrides=ov, p_extra=pe)
 
 
-def _check_grad(g_gpu, g_ref, tol=TOL):
-    scale = max(1.0, float(np.abs(g_ref).max()))
-    err = float(np.abs(g_gpu - g_ref).max())
-    assert err <= tol * scale, 'max |grad err| {} (scale {})'.format(err, scale)
+def _check_grad(g_gpu, g_ref, prob, tol=TOL):
+    """Per variable, each against its own largest reference component (_fixtures)."""
+    check_grad_per_var(g_gpu, g_ref, prob.layers, prob.d_in, tol)
 
 
 @pytest.mark.parametrize('name', list(CASES))
@@ -48,7 +47,7 @@ def test_web_matches_oracle(gpu, name):
     np.testing.assert_allclose(s, ref.s, rtol=TOL, atol=TOL)
     s2 = model.test_scores(batch, seed=seed)
     model.fwd_bwd(batch, seed=seed)
-    _check_grad(model.grad.cpu().numpy(), ref.grad_mse)
+    _check_grad(model.grad.cpu().numpy(), ref.grad_mse, prob)
     loss_mse = float(model.loss_buf[0].item())
     assert abs(loss_mse - ref.loss_mse) <= TOL * max(1.0, abs(ref.loss_mse))
     model.apply_adam()
@@ -71,7 +70,7 @@ def test_web_wide_types_and_k16(gpu):
     np.testing.assert_allclose(model.pred_sim_without_act(batch, seed=99).cpu().numpy(), ref.s,
                                rtol=TOL, atol=TOL)
     model.fwd_bwd(batch, seed=99)
-    _check_grad(model.grad.cpu().numpy(), ref.grad_mse)
+    _check_grad(model.grad.cpu().numpy(), ref.grad_mse, prob)
 
 
 def test_web_padding_value(gpu):
@@ -86,7 +85,7 @@ def test_web_padding_value(gpu):
     np.testing.assert_allclose(model.pred_sim_without_act(batch, seed=77).cpu().numpy(), ref.s,
                                rtol=TOL, atol=TOL)
     model.fwd_bwd(batch, seed=77)
-    _check_grad(model.grad.cpu().numpy(), ref.grad_mse)
+    _check_grad(model.grad.cpu().numpy(), ref.grad_mse, prob)
 
 
 def test_web_chunks_shards_determinism(gpu):
@@ -107,7 +106,7 @@ def test_web_chunks_shards_determinism(gpu):
     assert torch.equal(g_full, model.grad), 'sg_web_fwd_bwd is not bitwise reproducible'
     model.fwd_bwd(chunked, seed=seed)
     g = model.grad.cpu().numpy()
-    _check_grad(g, g_full.cpu().numpy(), tol=1e-5)
+    _check_grad(g, g_full.cpu().numpy(), prob, tol=1e-5)
     # shards of the pair list keyed by their global offset
     h = full.n_pairs // 2
     b0 = model.web_batch(full.csr, full.pairs[:h], full.labels[:h], 0, full.n_pairs,
@@ -120,7 +119,7 @@ def test_web_chunks_shards_determinism(gpu):
     model.fwd_bwd(b0, seed=seed, add_label_term=True)
     g0, l0 = model.grad.clone(), float(model.loss_buf[0].item())
     model.fwd_bwd(b1, seed=seed, add_label_term=False)
-    _check_grad((g0 + model.grad).cpu().numpy(), g_full.cpu().numpy(), tol=1e-5)
+    _check_grad((g0 + model.grad).cpu().numpy(), g_full.cpu().numpy(), prob, tol=1e-5)
     assert abs(l0 + float(model.loss_buf[0].item()) - l_full) <= 1e-5 * max(1.0, abs(l_full))
 
 

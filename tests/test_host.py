@@ -90,14 +90,18 @@ def test_packer_rejects_oversize_graph():
         GraphStore(prob.mgs, 10)
 
 
+@pytest.mark.parametrize('f64_acc', [False, True])
 @pytest.mark.parametrize('dropout', [0.0, 0.1])
-def test_c_restatement_matches_numpy_oracle(dropout):
+def test_c_restatement_matches_numpy_oracle(dropout, f64_acc):
+    """Both builds of the C restatement: float gradient sums (the timed CPU baseline) and
+    double sums (the full-batch GPU checker, tests/test_gpu_fullbatch.py)."""
     prob = small_problem(n_graphs=16, n_pairs=64, seed=21, flags_overrides=dict(dropout=dropout))
     ref = run_oracle_step(prob, 1234, adam=False)
     words = prob.store().pack_host(prob.pairs, prob.labels)
     ybar = prob.labels.astype(np.float64).mean()
     s, g, loss = cpu_ref.fwd_bwd_records(words, prob.n_max, prob.d_in, prob.params, 1234,
-                                         1 - dropout, prob.flags.yeta, ybar, threads=2)
+                                         1 - dropout, prob.flags.yeta, ybar, threads=2,
+                                         f64_acc=f64_acc)
     np.testing.assert_allclose(s, ref.s, rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(g, ref.grad_mse, rtol=1e-4, atol=1e-5)
     label_term = 0.5 * ((prob.labels.astype(np.float64) - ybar) ** 2).sum()
