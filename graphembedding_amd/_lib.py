@@ -126,6 +126,13 @@ def lib():
     L.sg_pair_order_workspace_bytes.restype = c_i64
     L.sg_pair_order.argtypes = [pm, vp, c_i64, vp, vp, vp]
     L.sg_pair_order.restype = c_i32
+    L.sg_pair_order_cls.argtypes = [pm, vp, c_i64, vp, vp, vp, vp]
+    L.sg_pair_order_cls.restype = c_i32
+    L.sg_forward_cls.argtypes = [pm, vp, vp, vp, c_i64, c_i64, vp, c_u64, vp, vp, vp]
+    L.sg_forward_cls.restype = c_i32
+    L.sg_fwd_bwd_cls.argtypes = [pm, vp, vp, vp, c_i64, c_i64, c_i64, vp, c_u64, vp, c_i32, vp,
+                                 vp, vp, vp, vp]
+    L.sg_fwd_bwd_cls.restype = c_i32
     L.sg_sampler_random.argtypes = [vp, vp, c_i32, c_i64, vp, vp]
     L.sg_sampler_random.restype = c_i32
     L.sg_sampler_density.argtypes = [vp, vp, vp, c_i32, c_i32, vp, c_i64, vp, vp]
@@ -173,7 +180,11 @@ EXPORTED_SYMBOLS = ('sg_version', 'sg_record_bytes', 'sg_record_bytes_ex', 'sg_m
                     'sg_pair_order_workspace_bytes', 'sg_sampler_random', 'sg_sampler_density',
                     'sg_adam_workspace_bytes', 'sg_adam_tf_ex', 'sg_web_workspace_bytes',
                     'sg_web_forward', 'sg_web_fwd_bwd', 'sg_fwd_bwd_dseed', 'sg_seed_advance',
-                    'sg_feed_step', 'sg_pair_order_src', 'sg_forward_src', 'sg_fwd_bwd_src')
+                    'sg_feed_step', 'sg_pair_order_src', 'sg_forward_src', 'sg_fwd_bwd_src',
+                    'sg_pair_order_cls', 'sg_forward_cls', 'sg_fwd_bwd_cls')
+
+# class_start entries of sg_pair_order_cls (include/siamese_hip.h SG_FAST_CLASSES_P1)
+FAST_CLASSES_P1 = 5
 
 # sg_dtype: storage type of Â in the pair records
 DTYPES = {'f32': 0, 'bf16': 1}
@@ -311,15 +322,39 @@ def pair_order(m: SgModel, records, n_pairs, order_out, workspace, stream=None):
                               _ptr(workspace), _stream(stream)), 'sg_pair_order')
 
 
+def pair_order_cls(m: SgModel, records, n_pairs, order_out, class_start, workspace,
+                   stream=None):
+    """sg_pair_order plus the class table (int32 [FAST_CLASSES_P1]) of the fused path."""
+    check(lib().sg_pair_order_cls(ctypes.byref(m), _ptr(records), int(n_pairs), _ptr(order_out),
+                                  _ptr(class_start), _ptr(workspace), _stream(stream)),
+          'sg_pair_order_cls')
+
+
 def forward(m: SgModel, records, n_pairs, pair_offset, params, seed, s_out, workspace=None,
-            stream=None, order=None):
+            stream=None, order=None, class_start=None):
+    if class_start is not None:
+        check(lib().sg_forward_cls(ctypes.byref(m), _ptr(records), _ptr(order),
+                                   _ptr(class_start), int(n_pairs), int(pair_offset),
+                                   _ptr(params), int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(s_out),
+                                   _ptr(workspace), _stream(stream)), 'sg_forward_cls')
+        return
     check(lib().sg_forward_ex(ctypes.byref(m), _ptr(records), _ptr(order), int(n_pairs),
                               int(pair_offset), _ptr(params), int(seed) & 0xFFFFFFFFFFFFFFFF,
                               _ptr(s_out), _ptr(workspace), _stream(stream)), 'sg_forward_ex')
 
 
 def fwd_bwd(m: SgModel, records, n_pairs, pair_offset, batch_total, params, seed, y_stats,
-            add_label_term, s_out, grad_out, loss_out, workspace, stream=None, order=None):
+            add_label_term, s_out, grad_out, loss_out, workspace, stream=None, order=None,
+            class_start=None):
+    if class_start is not None:
+        check(lib().sg_fwd_bwd_cls(ctypes.byref(m), _ptr(records), _ptr(order),
+                                   _ptr(class_start), int(n_pairs), int(pair_offset),
+                                   int(batch_total), _ptr(params),
+                                   int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(y_stats),
+                                   int(add_label_term), _ptr(s_out), _ptr(grad_out),
+                                   _ptr(loss_out), _ptr(workspace), _stream(stream)),
+              'sg_fwd_bwd_cls')
+        return
     check(lib().sg_fwd_bwd_ex(ctypes.byref(m), _ptr(records), _ptr(order), int(n_pairs),
                               int(pair_offset), int(batch_total), _ptr(params),
                               int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(y_stats), int(add_label_term),

@@ -55,6 +55,10 @@ DEFAULTS: Dict[str, Any] = dict(
     ntn_mode='reference',      # 'reference' = (ΣU)·Σ relu(m) quirk (A1) | 'intended'
     label_stream='compat',     # 'compat' = labels from a later sampler draw (A3) | 'aligned'
     test_matrix='full',        # 'full' = sim_mat[i][j] | 'compat_diag' = sim_mat[i][i] (A5)
+    # test_time_mat: 'batched' = one launch for all m x n pairs, every entry the launch time
+    # / (m n) (a deviation from the reference, recorded on the result); 'per_pair' = one
+    # timed single-pair launch per entry, as train.py:57-69 times each sess.run
+    test_time='batched',
     n_max=None,                # record node capacity (default: Padding max_in_dims or data max)
     record_dtype='f32',        # storage of Â in pair records: 'f32' | 'bf16' (config C3); fp32 math
     seed=123,                  # dropout RNG base seed (the reference's TF RNG was unseeded)

@@ -74,6 +74,12 @@ constexpr int MAXW = SG_FAST_MAXW;
 struct FastArgs {
   const uint8_t *recs;
   const int32_t *order;   // processing order (sg_pair_order) or null
+  // class table of the order (sg_pair_order_cls) or null: the order's slots
+  // [cls[c], cls[c + 1]) hold the records of cost class c = (N0 > 8) + 2 (N1 > 8); each
+  // wave then runs ONE class (its own loop: no register copies at a class join), the
+  // waves split over the classes by work (count x cost weight cw[c])
+  const int32_t *cls;
+  float cw[4];
   int64_t n_pairs;
   int64_t pair_offset;
   int rw4h;      // 16-B words per HBM record (f32 or bf16 Â)
@@ -265,13 +271,71 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   const int stride = (int)gridDim.x * nw;
   const int gw = (int)blockIdx.x * nw + wv;
   const int32_t *__restrict__ ord = A.order;
+  // Class-exclusive schedule (A.cls): wave gw takes class cwave and the slot range
+  // [cs0, cs1) of that class; every wave computes the same split (scalar code).  The
+  // waves are divided over the classes in proportion to count x cost weight (largest
+  // remainder), then each class's slots evenly over its waves.  Needs one wave per
+  // non-empty class; otherwise (tiny batches) the mixed schedule runs.
+  int cwave = -1, cs0 = 0, cs1 = 0;
+  if (ord != nullptr && A.cls != nullptr) {
+    int cb[5];
+#pragma unroll
+    for (int c = 0; c < 5; ++c) cb[c] = __builtin_amdgcn_readfirstlane(A.cls[c]);
+    float wt[4], tot = 0.f;
+    int nonempty = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int nc = cb[c + 1] - cb[c];
+      wt[c] = nc > 0 ? (float)nc * A.cw[c] : 0.f;
+      tot += wt[c];
+      nonempty += nc > 0;
+    }
+    if (nonempty > 0 && stride >= nonempty) {
+      int wc[4], used = 0;
+      float fr[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float x = wt[c] > 0.f ? (float)(stride - nonempty) * (wt[c] / tot) : 0.f;
+        const int fl = (int)x;
+        wc[c] = wt[c] > 0.f ? 1 + fl : 0;   // at least one wave per non-empty class
+        fr[c] = x - (float)fl;
+        used += wc[c];
+      }
+      for (int left = stride - used; left > 0; --left) {   // largest remainders, ties to low c
+        int bc = 0;
+        float bf = -1.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (wt[c] > 0.f && fr[c] > bf) {
+            bf = fr[c];
+            bc = c;
+          }
+        wc[bc] += 1;
+        fr[bc] = -2.f;
+      }
+      int cum = 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (cwave < 0 && gw < cum + wc[c]) {
+          const int k = gw - cum, nc = cb[c + 1] - cb[c];
+          cwave = c;
+          cs0 = cb[c] + (int)((int64_t)k * nc / wc[c]);
+          cs1 = cb[c] + (int)((int64_t)(k + 1) * nc / wc[c]);
+        }
+        cum += wc[c];
+      }
+    }
+  }
+  const bool cls_mode = cwave >= 0;
+  const int qend = cls_mode ? cs1 : npairs;   // slots of this wave run below qend
   auto slot_of = [&](int r) -> int {
+    if (cls_mode) return cs0 + r;
     return r * stride + ((ord != nullptr && (r & 1)) ? stride - 1 - gw : gw);
   };
   // record indices of 64 rounds, lane i ↔ round r0 + i (read back with readlane)
   auto load_ord = [&](int r0) -> int {
     const int s = slot_of(r0 + l);
-    return s < npairs ? ord[s] : 0;
+    return s < qend ? ord[s] : 0;
   };
   // an entry read back from ordA, clamped (scalar) so a bad order never reads out of bounds
   auto ord_at = [&](int v, int lane) -> int {
@@ -321,7 +385,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   for (int i = 8 * bdx + tid; i < nprm; i += bdx) stg[i] = prm[i];   // small blocks only
   // first record: its HBM latency overlaps the table build below
   int q = slot_of(0);
-  int p = (ord && q < npairs) ? ord_at(ordA, 0) : q;
+  int p = (ord && q < qend) ? ord_at(ordA, 0) : q;
   // HBM record: rw4h 16-B words (RW4 for f32 Â, fewer for bf16 Â)
   const int rw4h = A.rw4h;
   constexpr int ADJ4 = D * D / 4;   // 16-B words of a bf16 adjacency block (D even)
@@ -329,7 +393,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #pragma unroll
   for (int c = 0; c < NREC; ++c) {
     const int w4 = l + 64 * c;
-    pre[c] = (q < npairs && w4 < rw4h)
+    pre[c] = (q < qend && w4 < rw4h)
                  ? (SRC ? fast_store_word<D>(A, p, w4, l)
                                 : ((const uint4 *)(A.recs + (size_t)p * (size_t)rw4h * 16u))[w4])
                  : uint4{0u, 0u, 0u, 0u};
@@ -451,7 +515,12 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #endif
   int it = 0;
   const bool young = wv >= 4;
-  for (; q < npairs; ++it) {
+  // The pair loop: CLS < 0 = mixed schedule (each pair dispatches to its (K0, K1) body);
+  // CLS = c: every pair of this wave has class c, one body, so the loop-carried
+  // accumulators need no copies at a join of four bodies (≈55 v_mov_b32 per pair)
+  auto pair_loop = [&](auto CLSc) __attribute__((always_inline)) {
+  constexpr int CLS = decltype(CLSc)::value;
+  for (; q < qend; ++it) {
     const bool yturn = (it % SG_PRIO_PERIOD) < SG_PRIO_YOUNG;
     if (yturn == young) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
@@ -490,12 +559,12 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           ordA = ordB;
           ordB = load_ord(it + 65);
         }
-        pn = qn < npairs ? ord_at(ordA, rl) : 0;
+        pn = qn < qend ? ord_at(ordA, rl) : 0;
       }
 #pragma unroll
       for (int c = 0; c < NREC; ++c) {
         const int w4 = l + 64 * c;
-        if (qn < npairs && w4 < rw4h)
+        if (qn < qend && w4 < rw4h)
           pre[c] = SRC
                        ? fast_store_word<D>(A, pn, w4, l)
                        : ((const uint4 *)(A.recs + (size_t)pn * (size_t)rw4h * 16u))[w4];
@@ -998,18 +1067,32 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         }
       }
     };
-    const bool big0 = N0 > 8, big1 = N1 > 8;
-    if (big0) {
-      if (big1) body(std::integral_constant<int, 3>{}, std::integral_constant<int, 3>{});
-      else body(std::integral_constant<int, 3>{}, std::integral_constant<int, 2>{});
-    } else {
-      if (big1) body(std::integral_constant<int, 2>{}, std::integral_constant<int, 3>{});
-      else body(std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{});
+    if constexpr (CLS < 0) {
+      const bool big0 = N0 > 8, big1 = N1 > 8;
+      if (big0) {
+        if (big1) body(std::integral_constant<int, 3>{}, std::integral_constant<int, 3>{});
+        else body(std::integral_constant<int, 3>{}, std::integral_constant<int, 2>{});
+      } else {
+        if (big1) body(std::integral_constant<int, 2>{}, std::integral_constant<int, 3>{});
+        else body(std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{});
+      }
+    } else {   // the class table guarantees (N0 > 8, N1 > 8) == (CLS & 1, CLS & 2)
+      body(std::integral_constant<int, (CLS & 1) ? 3 : 2>{},
+           std::integral_constant<int, (CLS & 2) ? 3 : 2>{});
     }
+  }
+  };
+  if (cls_mode) {
+    if (cwave == 0) pair_loop(std::integral_constant<int, 0>{});
+    else if (cwave == 1) pair_loop(std::integral_constant<int, 1>{});
+    else if (cwave == 2) pair_loop(std::integral_constant<int, 2>{});
+    else pair_loop(std::integral_constant<int, 3>{});
+  } else {
+    pair_loop(std::integral_constant<int, -1>{});
   }
 
   SG_STAMP(2, __builtin_amdgcn_s_memrealtime());
-  SG_STAMP(4, (unsigned long long)it);
+  SG_STAMP(4, (unsigned long long)it | ((unsigned long long)(cwave + 1) << 32));
   if (!BWD) return;
   // ---- flush: every wave dumps its accumulator slots to LDS, all threads sum ----
   // Slot s of lane (g, j) maps to at most one parameter (fast_param below) and
@@ -1236,7 +1319,7 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
                 const int32_t *order, int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
                 uint64_t seed, const float *y_stats, float *s_out, float *slab, float *ntn,
                 int *blocks_out, hipStream_t stream, const uint64_t *seed_dev,
-                const sg_pair_source_t *src) {
+                const sg_pair_source_t *src, const int32_t *class_start) {
   const int D = P.n_max;
   FastCfg c = fast_cfg(P, n_pairs, bwd);
   // the kernel indexes pairs in 32 bits (2^31 records would be ≥ 1 TB)
@@ -1255,6 +1338,17 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
   if (src && (P.adj_dtype != SG_DTYPE_F32 || src->n_max != D || src->n_graphs <= 0))
     return SG_ERR_ARG;
   A.order = order;
+  A.cls = order ? class_start : nullptr;
+  // relative cost of a pair of class (N0 > 8) + 2 (N1 > 8): the class-exclusive schedule
+  // gives each class waves in proportion to count x cost (SG_CLS_W="w0,w1,w2,w3" to tune)
+  A.cw[0] = 1.f;
+  A.cw[1] = A.cw[2] = 1.31f;
+  A.cw[3] = 1.51f;
+  if (const char *ev = getenv("SG_CLS_W")) {
+    float w[4];
+    if (sscanf(ev, "%f,%f,%f,%f", &w[0], &w[1], &w[2], &w[3]) == 4)
+      for (int k = 0; k < 4; ++k) A.cw[k] = w[k] > 0.f ? w[k] : 1.f;
+  }
   A.n_pairs = n_pairs;
   A.rw4h = P.hbm_words / 4;
   A.rec_bf16 = P.adj_dtype == SG_DTYPE_BF16 ? 1 : 0;

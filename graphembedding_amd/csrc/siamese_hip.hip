@@ -37,7 +37,7 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
                 const int32_t *order, int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
                 uint64_t seed, const float *y_stats, float *s_out, float *slab, float *ntn,
                 int *blocks_out, hipStream_t stream, const uint64_t *seed_dev = nullptr,
-                const sg_pair_source_t *src = nullptr);
+                const sg_pair_source_t *src = nullptr, const int32_t *class_start = nullptr);
 // fused capacity-32 path (sg_fast32.hip)
 int sg_fast32_supported(const sg_model_t *m, const SgGenPlan &P);
 // graph-store path for Web-sized graphs (sg_web.hip)
@@ -243,9 +243,10 @@ __device__ __forceinline__ int sg_order_key(const S &src, int64_t p, int nmax, i
   src.n01(p, n0, n1);
   n0 = n0 < 0 ? 0 : (n0 > nmax ? nmax : n0);
   n1 = n1 < 0 ? 0 : (n1 > nmax ? nmax : n1);
-  // fast: 1 = sg_fast (third k-step per side), 2 = sg_fast32 (k-blocks of 4 nodes)
+  // fast: 1 = sg_fast: class (N0 > 8) + 2 (N1 > 8), the kernel's four (K0, K1) bodies
+  // (third Â k-step per side); 2 = sg_fast32 (k-blocks of 4 nodes)
   if (fast == 2) return ((n0 + 3) >> 2) + ((n1 + 3) >> 2);
-  return fast ? (n0 > 8) + (n1 > 8) : n0 + n1;
+  return fast ? (n0 > 8) + 2 * (n1 > 8) : n0 + n1;
 }
 
 template <class S>
@@ -323,6 +324,15 @@ __global__ void __launch_bounds__(256) sg_order_scatter(S src, int64_t n, int nm
     for (int k = t; k < K; k += blockDim.x) run[k] += wc[0][k] + wc[1][k] + wc[2][k] + wc[3][k];
     __syncthreads();
   }
+}
+
+// class table of an order: class_start[k] = first slot of key k (the exclusive scan of
+// the key-major counts at chunk 0), class_start[K] = n
+__global__ void sg_order_starts(const int32_t *__restrict__ base, int K, int nb, int64_t n,
+                                int32_t *__restrict__ class_start) {
+  const int k = threadIdx.x;
+  if (k < K) class_start[k] = base[(size_t)k * nb];
+  if (k == K) class_start[K] = (int32_t)n;
 }
 
 // ---- TF ApplyAdam (+ weight decay gradient) in one workgroup ----
@@ -489,7 +499,7 @@ int64_t ntn_offset_floats(const PathChoice &c, int64_t n_pairs) {
 // ===========================================================================
 extern "C" {
 
-int32_t sg_version(void) { return 10600; }   /* 1.6.0: store-sourced pairs (sg_*_src) */
+int32_t sg_version(void) { return 10700; }   /* 1.7.0: class-exclusive schedule (sg_*_cls) */
 
 int64_t sg_record_bytes(int32_t n_max) { return sg_record_bytes_ex(n_max, SG_DTYPE_F32); }
 
@@ -588,8 +598,8 @@ int64_t sg_pair_order_workspace_bytes(const sg_model_t *model, int64_t n_pairs) 
 
 extern "C++" template <class S>
 static int32_t launch_order(S src, int nmax, int fast, int64_t n_pairs, int32_t *order_out,
-                            void *workspace, hipStream_t st) {
-  const int K = fast == 1 ? 3 : (fast == 2 ? 2 * ((nmax + 3) / 4) + 1 : 2 * nmax + 1);
+                            void *workspace, hipStream_t st, int32_t *class_start = nullptr) {
+  const int K = fast == 1 ? 4 : (fast == 2 ? 2 * ((nmax + 3) / 4) + 1 : 2 * nmax + 1);
   const int nb = (int)((n_pairs + kOrderChunk - 1) / kOrderChunk);
   int32_t *cnt = (int32_t *)workspace;
   hipLaunchKernelGGL(sg_order_count<S>, dim3(nb), dim3(256), 0, st, src, n_pairs, nmax, fast, K,
@@ -597,6 +607,9 @@ static int32_t launch_order(S src, int nmax, int fast, int64_t n_pairs, int32_t 
   hipLaunchKernelGGL(sg_order_scan, dim3(1), dim3(1024), 0, st, cnt, (int64_t)K * nb);
   hipLaunchKernelGGL(sg_order_scatter<S>, dim3(nb), dim3(256), 0, st, src, n_pairs, nmax, fast, K,
                      nb, (const int32_t *)cnt, order_out);
+  if (class_start)
+    hipLaunchKernelGGL(sg_order_starts, dim3(1), dim3(256), 0, st, (const int32_t *)cnt, K, nb,
+                       n_pairs, class_start);
   return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
 }
 
@@ -611,6 +624,25 @@ int32_t sg_pair_order(const sg_model_t *model, const void *records, int64_t n_pa
   const SgRecLayout rl = sg_rec_layout(nmax, c.plan.adj_dtype);
   OrderRecs src{(const uint8_t *)records, rl.words, rl.adj_words + 2 * nmax};
   return launch_order(src, nmax, c.path, n_pairs, order_out, workspace, (hipStream_t)stream);
+}
+
+int32_t sg_pair_order_cls(const sg_model_t *model, const void *records, int64_t n_pairs,
+                          int32_t *order_out, int32_t *class_start, void *workspace,
+                          sg_stream_t stream) {
+  if (n_pairs < 0 || n_pairs > 0x7FFFFFFF) return SG_ERR_ARG;
+  if (!class_start) return SG_ERR_ARG;
+  PathChoice c = choose_path(model, true);
+  if (c.status != SG_OK) return c.status;
+  if (c.path != 1) return SG_ERR_UNSUPPORTED;   // the class-exclusive schedule is sg_fast's
+  hipStream_t st = (hipStream_t)stream;
+  if (n_pairs == 0)
+    return hipMemsetAsync(class_start, 0, SG_FAST_CLASSES_P1 * 4u, st) == hipSuccess ? SG_OK
+                                                                                     : SG_ERR_HIP;
+  if (!records || !order_out || !workspace) return SG_ERR_ARG;
+  const int nmax = c.plan.n_max;
+  const SgRecLayout rl = sg_rec_layout(nmax, c.plan.adj_dtype);
+  OrderRecs src{(const uint8_t *)records, rl.words, rl.adj_words + 2 * nmax};
+  return launch_order(src, nmax, 1, n_pairs, order_out, workspace, st, class_start);
 }
 
 // a store-sourced call's checks: fused capacity-32 path, f32 Â, store shape = n_max
@@ -643,25 +675,46 @@ int32_t sg_forward(const sg_model_t *model, const void *records, int64_t n_pairs
                        workspace, stream);
 }
 
-int32_t sg_forward_ex(const sg_model_t *model, const void *records, const int32_t *order,
-                      int64_t n_pairs, int64_t pair_offset, const float *params, uint64_t seed,
-                      float *s_out, void *workspace, sg_stream_t stream) {
-  (void)workspace;
+static int32_t forward_impl(const sg_model_t *model, const void *records, const int32_t *order,
+                            const int32_t *class_start, int64_t n_pairs, int64_t pair_offset,
+                            const float *params, uint64_t seed, float *s_out,
+                            sg_stream_t stream) {
   if (n_pairs < 0 || pair_offset < 0) return SG_ERR_ARG;
   if (order && n_pairs > 0x7FFFFFFF) return SG_ERR_ARG;
+  if (class_start && !order) return SG_ERR_ARG;
   if (n_pairs == 0) return SG_OK;
   if (!records || !params || !s_out) return SG_ERR_ARG;
   PathChoice c = choose_path(model, false);
   if (c.status != SG_OK) return c.status;
+  if (class_start && c.path != 1) return SG_ERR_UNSUPPORTED;
   if (c.path == 1)
     return sg_fast_run(model, c.plan, false, records, order, n_pairs, pair_offset, n_pairs, params,
-                       seed, nullptr, s_out, nullptr, nullptr, nullptr, (hipStream_t)stream);
+                       seed, nullptr, s_out, nullptr, nullptr, nullptr, (hipStream_t)stream,
+                       nullptr, nullptr, class_start);
   if (c.path == 2)
     return sg_fast32_run(model, c.plan, false, records, order, n_pairs, pair_offset, n_pairs,
                          params, seed, nullptr, s_out, nullptr, nullptr, nullptr,
                          (hipStream_t)stream);
   return sg_generic_run(c.plan, false, records, order, n_pairs, pair_offset, n_pairs, params, seed,
                         nullptr, s_out, nullptr, nullptr, (hipStream_t)stream);
+}
+
+int32_t sg_forward_ex(const sg_model_t *model, const void *records, const int32_t *order,
+                      int64_t n_pairs, int64_t pair_offset, const float *params, uint64_t seed,
+                      float *s_out, void *workspace, sg_stream_t stream) {
+  (void)workspace;
+  return forward_impl(model, records, order, nullptr, n_pairs, pair_offset, params, seed, s_out,
+                      stream);
+}
+
+int32_t sg_forward_cls(const sg_model_t *model, const void *records, const int32_t *order,
+                       const int32_t *class_start, int64_t n_pairs, int64_t pair_offset,
+                       const float *params, uint64_t seed, float *s_out, void *workspace,
+                       sg_stream_t stream) {
+  (void)workspace;
+  if (!order || !class_start) return SG_ERR_ARG;
+  return forward_impl(model, records, order, class_start, n_pairs, pair_offset, params, seed,
+                      s_out, stream);
 }
 
 int32_t sg_fwd_bwd(const sg_model_t *model, const void *records, int64_t n_pairs,
@@ -677,9 +730,11 @@ static int32_t fwd_bwd_impl(const sg_model_t *model, const void *records, const 
                             const float *params, uint64_t seed, const uint64_t *seed_dev,
                             const float *y_stats, int32_t add_label_term, float *s_out,
                             float *grad_out, float *loss_out, void *workspace,
-                            sg_stream_t stream, const sg_pair_source_t *src = nullptr) {
+                            sg_stream_t stream, const sg_pair_source_t *src = nullptr,
+                            const int32_t *class_start = nullptr) {
   if (n_pairs < 0 || pair_offset < 0) return SG_ERR_ARG;
   if (order && n_pairs > 0x7FFFFFFF) return SG_ERR_ARG;
+  if (class_start && !order) return SG_ERR_ARG;
   if (!params || !grad_out || !workspace) return SG_ERR_ARG;
   PathChoice c = choose_path(model, true);
   if (c.status != SG_OK) return c.status;
@@ -688,6 +743,7 @@ static int32_t fwd_bwd_impl(const sg_model_t *model, const void *records, const 
     if (rc != SG_OK) return rc;
   }
   if (seed_dev && c.path != 1) return SG_ERR_UNSUPPORTED;   // device seed: fused path only
+  if (class_start && c.path != 1) return SG_ERR_UNSUPPORTED;   // class table: sg_fast only
   if (model->loss_mode == SG_LOSS_BROADCAST && !y_stats) return SG_ERR_ARG;
   if (model->loss_mode == SG_LOSS_ALIGNED && batch_total <= 0) return SG_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
@@ -705,7 +761,7 @@ static int32_t fwd_bwd_impl(const sg_model_t *model, const void *records, const 
   if (c.path == 1)
     rc = sg_fast_run(model, c.plan, true, records, order, n_pairs, pair_offset, batch_total,
                      params, seed, y_stats, s_out, slab, slab + ntn_offset_floats(c, n_pairs),
-                     &nblk, st, seed_dev, src);
+                     &nblk, st, seed_dev, src, class_start);
   else if (c.path == 2)
     rc = sg_fast32_run(model, c.plan, true, records, order, n_pairs, pair_offset, batch_total,
                        params, seed, y_stats, s_out, slab, slab + ntn_offset_floats(c, n_pairs),
@@ -727,6 +783,17 @@ int32_t sg_fwd_bwd_ex(const sg_model_t *model, const void *records, const int32_
   return fwd_bwd_impl(model, records, order, n_pairs, pair_offset, batch_total, params, seed,
                       nullptr, y_stats, add_label_term, s_out, grad_out, loss_out, workspace,
                       stream);
+}
+
+int32_t sg_fwd_bwd_cls(const sg_model_t *model, const void *records, const int32_t *order,
+                       const int32_t *class_start, int64_t n_pairs, int64_t pair_offset,
+                       int64_t batch_total, const float *params, uint64_t seed,
+                       const float *y_stats, int32_t add_label_term, float *s_out,
+                       float *grad_out, float *loss_out, void *workspace, sg_stream_t stream) {
+  if (!order || !class_start) return SG_ERR_ARG;
+  return fwd_bwd_impl(model, records, order, n_pairs, pair_offset, batch_total, params, seed,
+                      nullptr, y_stats, add_label_term, s_out, grad_out, loss_out, workspace,
+                      stream, nullptr, class_start);
 }
 
 int32_t sg_fwd_bwd_src(const sg_model_t *model, const sg_pair_source_t *src,

@@ -82,6 +82,7 @@ class Batch:
     batch_total: int = 0            # global batch size B
     gid_pairs: Optional[np.ndarray] = None
     order: object = None            # torch.int32 [n] processing order (balance()) or None
+    cls: object = None              # torch.int32 [5] class table of the order (fused path)
     # graph-store path (kernel path 3, config C5): pair ids into a CSR store instead of records
     csr: object = None              # web.CsrStore
     pairs: object = None            # torch.int32 [n, 2] store graph ids
@@ -187,7 +188,7 @@ class SiameseGCNTNMSE(object):
                              self._seed(seed), s, order=batch.order)
             return s
         _lib.forward(self.sg, batch.records, batch.n_pairs, batch.pair_offset, self.params,
-                     self._seed(seed), s, order=batch.order)
+                     self._seed(seed), s, order=batch.order, class_start=batch.cls)
         return s
 
     def get_feed_dict(self, data, dist_calculator, tvt, test_id=None, train_id=None):
@@ -369,22 +370,35 @@ class SiameseGCNTNMSE(object):
         _lib.fwd_bwd(self.sg, batch.records, batch.n_pairs, batch.pair_offset,
                      batch.batch_total, self.params, self._seed(seed), batch.y_stats,
                      1 if add_label_term else 0, s_out, self.grad, self.loss_buf,
-                     self.workspace(batch.n_pairs), order=batch.order)
+                     self.workspace(batch.n_pairs), order=batch.order, class_start=batch.cls)
 
-    def balance(self, batch: Batch) -> Batch:
+    # SG_CLASS_SCHEDULE=0 keeps the mixed (snake) schedule on the fused path
+    CLASS_SCHEDULE = True
+
+    def balance(self, batch: Batch, classes: Optional[bool] = None) -> Batch:
         """Attach the class-sorted processing order of the batch's records
         (sg_pair_order): every wavefront then gets the same mix of cheap and
-        expensive pairs.  Scores are unchanged; the gradient differs only by
-        summation order.  Worth it for batches that are stepped repeatedly
-        (all-pairs epochs), not for the reference's B = 5 feeds."""
+        expensive pairs.  On the fused path (kernel path 1) the order comes with its
+        class table (sg_pair_order_cls) and every wavefront runs the pairs of one class
+        (class-exclusive schedule).  Scores are unchanged; the gradient differs only by
+        summation order.  Worth it for batches that are stepped repeatedly (all-pairs
+        epochs), not for the reference's B = 5 feeds."""
+        import os
         torch = self.torch
         if batch.n_pairs == 0 or batch.csr is not None:
             return batch
+        if classes is None:
+            classes = self.CLASS_SCHEDULE and os.environ.get('SG_CLASS_SCHEDULE', '1') != '0'
         ws = torch.empty(_lib.pair_order_workspace_bytes(self.sg, batch.n_pairs) // 4 + 1,
                          dtype=torch.int32, device=self.device)
         order = torch.empty(batch.n_pairs, dtype=torch.int32, device=self.device)
+        batch.cls = None
         if batch.src is not None:
             _lib.pair_order_src(self.sg, batch.src, batch.n_pairs, order, ws)
+        elif classes and self.kernel_path == 1:
+            cls = torch.empty(_lib.FAST_CLASSES_P1, dtype=torch.int32, device=self.device)
+            _lib.pair_order_cls(self.sg, batch.records, batch.n_pairs, order, cls, ws)
+            batch.cls = cls
         else:
             _lib.pair_order(self.sg, batch.records, batch.n_pairs, order, ws)
         batch.order = order

@@ -83,7 +83,25 @@ def test(data, dist_calculator, model, flags=None, evaluator=None, verbose=True)
     _sync()
     elapsed = _time.time() - t0
     sims = np.asarray(model.apply_final_act_np(s), dtype=np.float64).reshape(m, n)
-    time_mat = np.full((m, n), elapsed * 1000.0 / max(1, m * n))   # msec per pair
+    time_mode = getattr(f, 'test_time', 'batched')
+    if time_mode == 'per_pair':
+        # train.py:57-69: every (i, j) timed around its own single-pair run (msec); the
+        # same dropout keys as the batched launch (pair index i * n + j), so the scores
+        # equal the batched ones
+        time_mat = np.zeros((m, n))
+        for i in range(m):
+            for j in range(n):
+                one = model.make_batch([g1s[i * n + j]], [g2s[i * n + j]], pair_offset=i * n + j,
+                                       batch_total=m * n)
+                _sync()
+                t = _time.time()
+                model.test_scores(one)
+                _sync()
+                time_mat[i][j] = (_time.time() - t) * 1000.0
+    elif time_mode == 'batched':
+        time_mat = np.full((m, n), elapsed * 1000.0 / max(1, m * n))   # msec per pair
+    else:
+        raise RuntimeError('Unknown test_time {}'.format(time_mode))
     if f.test_matrix == 'compat_diag':
         sim_mat = np.zeros((m, n))
         for i in range(m):
@@ -93,6 +111,9 @@ def test(data, dist_calculator, model, flags=None, evaluator=None, verbose=True)
     results = None
     if evaluator is not None:
         results = evaluator.eval_test(f.model, sim_mat, time_mat)
+        # the deviation is stated on the result: 'batched' entries are a launch average
+        results['time_mat_mode'] = {f.model: time_mode}
+        evaluator.rs[f.model].time_mat_mode = time_mode
     if verbose:
         print('scored {}x{} pairs in {}'.format(m, n, print_msec(elapsed)))
     return sim_mat, time_mat, results

@@ -229,6 +229,32 @@ int32_t sg_fwd_bwd_ex(const sg_model_t *model, const void *records, const int32_
                       void *workspace, sg_stream_t stream);
 
 /*
+ * Class-exclusive schedule (library 1.7; fused path, sg_model_validate path 1 only,
+ * else SG_ERR_UNSUPPORTED).  sg_pair_order_cls writes the order of sg_pair_order and
+ * class_start[0 .. SG_FAST_CLASSES_P1): the order's slots [class_start[c],
+ * class_start[c + 1]) hold the records of cost class c = (N0 > 8) + 2 (N1 > 8),
+ * class_start[4] = n_pairs.  sg_forward_cls / sg_fwd_bwd_cls then give every
+ * wavefront the slots of ONE class, so it runs one specialised pair body for the whole
+ * launch (no register copies where the four class bodies would join); the classes
+ * get wavefronts in proportion to their work.  Results equal sg_*_ex on the same
+ * order: scores bitwise, the gradient up to summation order.  class_start must come
+ * from sg_pair_order_cls on the same records and order (a wrong table drops nodes).
+ */
+#define SG_FAST_CLASSES_P1 5
+int32_t sg_pair_order_cls(const sg_model_t *model, const void *records, int64_t n_pairs,
+                          int32_t *order_out, int32_t *class_start, void *workspace,
+                          sg_stream_t stream);
+int32_t sg_forward_cls(const sg_model_t *model, const void *records, const int32_t *order,
+                       const int32_t *class_start, int64_t n_pairs, int64_t pair_offset,
+                       const float *params, uint64_t seed, float *s_out, void *workspace,
+                       sg_stream_t stream);
+int32_t sg_fwd_bwd_cls(const sg_model_t *model, const void *records, const int32_t *order,
+                       const int32_t *class_start, int64_t n_pairs, int64_t pair_offset,
+                       int64_t batch_total, const float *params, uint64_t seed,
+                       const float *y_stats, int32_t add_label_term, float *s_out,
+                       float *grad_out, float *loss_out, void *workspace, sg_stream_t stream);
+
+/*
  * Graph-captured training steps (library 1.5).  sg_fwd_bwd_ex with the dropout seed
  * read from device memory at kernel time, so one hipGraph capture of a step
  * (feed → fwd_bwd → Adam → sg_seed_advance) replays with a new seed each time: the

@@ -60,7 +60,8 @@ def main():
         # only the last launch: stamps of earlier launches were overwritten wave by wave
         t0 = T[:, 0].min()
         us = (T[:, :4] - t0) / 100.0       # 100 MHz -> µs
-        pairs = T[:, 4]
+        pairs = T[:, 4] & 0xFFFFFFFF
+        wcls = (T[:, 4] >> 32) - 1   # class of a class-exclusive wave, -1 = mixed schedule
         nwv = len(T)
         print('W={} pairs={} waves={} pairs/wave {}'.format(W, shard.n, nwv, stats(pairs)))
         print('  start      ', stats(us[:, 0]))
@@ -71,6 +72,17 @@ def main():
         print('  end        ', stats(us[:, 3]))
         per_pair = (us[:, 2] - us[:, 1]) / np.maximum(pairs, 1)
         print('  µs/pair/wave', stats(per_pair))
+        if (wcls >= 0).any():   # class-exclusive schedule: cost per class -> SG_CLS_W
+            base = None
+            for c in range(4):
+                sel = wcls == c
+                if not sel.any():
+                    continue
+                med = float(np.median(per_pair[sel]))
+                base = base or med
+                print('  class {} ({}{}) waves {:5d} µs/pair {}  rel {:.3f}  loop end {}'.format(
+                    c, 3 if c & 1 else 2, 3 if c & 2 else 2, int(sel.sum()),
+                    stats(per_pair[sel]), med / base, stats(us[sel, 2])))
         # blocks go round-robin over the 8 XCDs: block b -> XCD b % 8
         nwpb = 8
         blk = np.arange(nwv) // nwpb

@@ -42,3 +42,20 @@ def test_allpairs_training_reduces_loss(gpu):
     losses = [model.train_step(batch) for _ in range(40)]
     torch.cuda.synchronize()
     assert losses[-1] < losses[0], losses[::8]
+
+
+def test_per_pair_test_times(gpu):
+    """test_time='per_pair': every test-matrix entry timed around its own single-pair run,
+    as train.py:57-69 times each sess.run; 'batched' states its launch average on the
+    result (time_mat_mode)."""
+    from graphembedding_amd.config import Flags
+    from graphembedding_amd.train import main
+    f = Flags(dataset='syn_aids80nef', iters=1, n_max=10, test_time='per_pair')
+    _, (sim_mat, time_mat, results) = main(f, device=gpu)
+    assert time_mat.shape == (10, 70) and np.all(time_mat > 0)
+    assert len(np.unique(time_mat)) > 1
+    assert results['time_mat_mode'] == {f.model: 'per_pair'}
+    f2 = Flags(dataset='syn_aids80nef', iters=1, n_max=10)
+    _, (sim2, time2, res2) = main(f2, device=gpu)
+    assert res2['time_mat_mode'] == {f2.model: 'batched'}
+    assert len(np.unique(time2)) == 1

@@ -1,4 +1,5 @@
-"""Processing order (sg_pair_order, sg_forward_ex / sg_fwd_bwd_ex; include/siamese_hip.h).
+"""Processing order (sg_pair_order, sg_forward_ex / sg_fwd_bwd_ex; include/siamese_hip.h)
+and the class-exclusive schedule (sg_pair_order_cls, sg_forward_cls / sg_fwd_bwd_cls).
 
 sg_pair_order must be the stable sort of the records by cost class, and walking
 it must change nothing but the gradient's summation order: scores bit-identical,
@@ -21,7 +22,7 @@ def _node_counts(prob):
 
 def _expected_order(prob, fused):
     n0, n1 = _node_counts(prob)
-    key = (n0 > 8).astype(int) + (n1 > 8).astype(int) if fused else n0 + n1
+    key = (n0 > 8).astype(int) + 2 * (n1 > 8).astype(int) if fused else n0 + n1
     return np.argsort(key, kind='stable').astype(np.int32)
 
 
@@ -105,3 +106,55 @@ def test_order_edge_cases(gpu):
     model.fwd_bwd(batch, seed=1)
     torch.cuda.synchronize()
     assert bool(torch.isfinite(model.grad).all())
+
+
+@pytest.mark.parametrize('n_pairs', [3, 37, 5000, 20011])
+def test_class_schedule_equals_mixed_schedule(gpu, n_pairs):
+    """sg_pair_order_cls's class table is the stable sort's class boundaries; the
+    class-exclusive schedule (each wave runs one class's pair body) gives the mixed
+    schedule's scores bit for bit, its gradient up to summation order, is bitwise
+    reproducible, and matches the oracle."""
+    import torch
+    prob = small_problem(n_graphs=40, n_pairs=n_pairs, seed=n_pairs, n_lo=3, n_hi=10)
+    model, batch = prob.make_gpu_model(device=gpu)
+    assert model.kernel_path == 1
+    seed = 4242
+    model.balance(batch, classes=False)
+    assert batch.cls is None
+    s_mix = model.pred_sim_without_act(batch, seed=seed).cpu().numpy()
+    model.fwd_bwd(batch, seed=seed)
+    g_mix = model.grad.cpu().numpy()
+    l_mix = float(model.loss_buf[0].item())
+    model.balance(batch, classes=True)
+    assert batch.cls is not None
+    n0, n1 = _node_counts(prob)
+    key = (n0 > 8).astype(int) + 2 * (n1 > 8).astype(int)
+    expect = np.concatenate([[0], np.cumsum(np.bincount(key, minlength=4))])
+    assert batch.cls.cpu().tolist() == expect.tolist()
+    assert np.array_equal(batch.order.cpu().numpy(), _expected_order(prob, True))
+    s_cls = model.pred_sim_without_act(batch, seed=seed).cpu().numpy()
+    assert np.array_equal(s_cls, s_mix)
+    s_out = torch.full((batch.n_pairs,), float('nan'), dtype=torch.float32, device=gpu)
+    model.fwd_bwd(batch, seed=seed, s_out=s_out)
+    assert np.array_equal(s_out.cpu().numpy(), s_mix)
+    g_cls = model.grad.clone()
+    scale = max(1.0, float(np.abs(g_mix).max()))
+    assert float(np.abs(g_cls.cpu().numpy() - g_mix).max()) <= 1e-5 * scale
+    assert abs(float(model.loss_buf[0].item()) - l_mix) <= 1e-5 * max(1.0, abs(l_mix))
+    model.fwd_bwd(batch, seed=seed)
+    assert torch.equal(g_cls, model.grad), 'class-schedule fwd_bwd is not bitwise reproducible'
+    if n_pairs <= 40:
+        ref = run_oracle_step(prob, seed)
+        np.testing.assert_allclose(s_cls, ref.s, rtol=TOL, atol=TOL)
+        from _fixtures import check_grad_per_var
+        check_grad_per_var(g_cls.cpu().numpy(), ref.grad_mse, prob.layers, prob.d_in, TOL)
+
+
+def test_class_table_needs_the_fused_path(gpu):
+    """sg_pair_order_cls is the fused path's (path 1); other paths keep the plain order."""
+    prob = small_problem(n_graphs=12, n_pairs=200, seed=5,
+                         flags_overrides=dict(AVERAGE_STACK, layer_2='Attention:input_dim=16'))
+    model, batch = prob.make_gpu_model(device=gpu)
+    assert model.kernel_path == 0
+    model.balance(batch)
+    assert batch.order is not None and batch.cls is None
