@@ -1341,9 +1341,11 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
   A.cls = order ? class_start : nullptr;
   // relative cost of a pair of class (N0 > 8) + 2 (N1 > 8): the class-exclusive schedule
   // gives each class waves in proportion to count x cost (SG_CLS_W="w0,w1,w2,w3" to tune)
+  // (measured per-class µs/pair, scripts/fast_timing.py, profiles/r03_tim: 1, 1.29, 1.31, 1.47)
   A.cw[0] = 1.f;
-  A.cw[1] = A.cw[2] = 1.31f;
-  A.cw[3] = 1.51f;
+  A.cw[1] = 1.29f;
+  A.cw[2] = 1.31f;
+  A.cw[3] = 1.47f;
   if (const char *ev = getenv("SG_CLS_W")) {
     float w[4];
     if (sscanf(ev, "%f,%f,%f,%f", &w[0], &w[1], &w[2], &w[3]) == 4)

@@ -49,6 +49,7 @@ constexpr int MKS = 20;             // MK LDS tile row stride (16 + 4): conflict
 constexpr int KMS = TB + 4;         // KM LDS tile row stride
 constexpr int HSLAB = 1 + 2 * WKP;  // head slab row: loss | gU[16] | gb[16]
 constexpr int WSPLIT = 8;           // split-K over pairs of the weight-gradient GEMMs
+constexpr int kUnitChunk = 4096;    // instances per block of the size-class sort (web_icls_*)
 
 struct WebPlan {
   int d_in, D, Dp, K;
@@ -133,6 +134,7 @@ int web_plan(const sg_model_t *m, WebPlan *W) {
 struct WebWs {
   int64_t Cp;                                        // chunk rounded up to TB
   int64_t X, GX, T, GM, EXT, EXT16, EXT128, INST;    // per-chunk buffers
+  int64_t ISORT, ICNT, ICLS;                         // instance units (web_icls_*)
   int64_t Wg, Wh, GWS, GVS, GSLAB, HSLABo, total;    // per-call buffers
   int gcn_blocks, head_blocks;
 };
@@ -155,6 +157,9 @@ WebWs web_ws(const WebPlan &W, int64_t chunk) {
   w.EXT16 = take(2 * (w.Cp / 16));
   w.EXT128 = take(2 * (w.Cp / TB));
   w.INST = take(8 * w.Cp);          // int4 per instance
+  w.ISORT = take(2 * w.Cp);         // instances sorted by size class
+  w.ICNT = take(3 * ((2 * w.Cp + kUnitChunk - 1) / kUnitChunk));
+  w.ICLS = take(4);
   w.Wg = take(K * Dp * Dp);
   w.Wh = take(K * Dp * Dp);
   w.GWS = take((int64_t)WSPLIT * K * Dp * Dp);
@@ -212,6 +217,82 @@ __global__ void __launch_bounds__(TB) web_ext_kernel(const int32_t *__restrict__
 }
 
 // ---------------------------------------------------------------------------
+// Instance size classes for the instance kernels' units (GcnArgs::isorted): a stable
+// counting sort of the chunk's instances by class (0: N <= cap4, 1: N <= cap2, 2: the
+// rest; cap4 / cap2 = a quarter / half of the instance region).  Blocks own contiguous
+// runs of kUnitChunk instances; counts are key-major so one exclusive scan gives every
+// (class, run) its base; the scatter ranks by ballot: deterministic.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int web_icls(const int4 *inst, int64_t q, int cap4, int cap2) {
+  const int N = inst[q].y;
+  return N <= cap4 ? 0 : (N <= cap2 ? 1 : 2);
+}
+
+__global__ void __launch_bounds__(256) web_icls_count(const int4 *__restrict__ inst, int64_t n,
+                                                      int cap4, int cap2, int nb,
+                                                      int32_t *__restrict__ cnt) {
+  __shared__ int h[3];
+  if (threadIdx.x < 3) h[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t b0 = (int64_t)blockIdx.x * kUnitChunk;
+  for (int i = threadIdx.x; i < kUnitChunk && b0 + i < n; i += blockDim.x)
+    atomicAdd(&h[web_icls(inst, b0 + i, cap4, cap2)], 1);
+  __syncthreads();
+  if (threadIdx.x < 3) cnt[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
+}
+
+// exclusive scan of the 3 nb counts (small: one thread), and the class starts
+__global__ void web_icls_scan(int32_t *__restrict__ cnt, int nb, int64_t n,
+                              int32_t *__restrict__ icls) {
+  if (threadIdx.x != 0) return;
+  int run = 0;
+  for (int k = 0; k < 3; ++k) {
+    icls[k] = run;
+    for (int b = 0; b < nb; ++b) {
+      const int v = cnt[(size_t)k * nb + b];
+      cnt[(size_t)k * nb + b] = run;
+      run += v;
+    }
+  }
+  icls[3] = (int32_t)n;
+}
+
+__global__ void __launch_bounds__(256) web_icls_scatter(const int4 *__restrict__ inst, int64_t n,
+                                                        int cap4, int cap2, int nb,
+                                                        const int32_t *__restrict__ base,
+                                                        int32_t *__restrict__ sorted) {
+  __shared__ int run[3];
+  __shared__ int wc[4][3];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t < 3) run[t] = base[(size_t)t * nb + blockIdx.x];
+  const int64_t b0 = (int64_t)blockIdx.x * kUnitChunk;
+  const int64_t b1 = b0 + kUnitChunk < n ? b0 + kUnitChunk : n;
+  for (int64_t t0 = b0; t0 < b1; t0 += 256) {
+    if (t < 12) (&wc[0][0])[t] = 0;
+    __syncthreads();
+    const int64_t q = t0 + t;
+    const bool valid = q < b1;
+    const int key = valid ? web_icls(inst, q, cap4, cap2) : -1;
+    int rank = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const uint64_t m = __ballot(valid && key == k);
+      if (key == k) rank = __popcll(m & ((1ull << lane) - 1ull));
+      if (lane == 0) wc[w][k] = __popcll(m);
+    }
+    __syncthreads();
+    if (valid) {
+      int off = run[key] + rank;
+      for (int v = 0; v < w; ++v) off += wc[v][key];
+      sorted[off] = (int32_t)q;
+    }
+    __syncthreads();
+    if (t < 3) run[t] += wc[0][t] + wc[1][t] + wc[2][t] + wc[3][t];
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Weight layouts for the GEMMs: Wg[k][a][b] = W[a][b][k] (T: rows a, contraction b)
 // and Wh[k][b][a] (gx2: rows b, contraction a); zero beyond D.
 // ---------------------------------------------------------------------------
@@ -265,6 +346,14 @@ struct GcnArgs {
   const float *val;
   const int32_t *pairs;
   const int4 *inst;  // [2 n_pairs] (first node, nodes, first Â entry, Â entries) per instance
+  // Units (web_units): the chunk's instances stable-sorted by size class (isorted) with
+  // the class starts icls[0..3] (class 0: N <= cap/4, 1: N <= cap/2, 2: larger; cap =
+  // the instance region of n_max nodes).  A workgroup takes a unit of 4, 2 or 1
+  // instances of one class and gives each a quarter / half / all of its waves and of
+  // its instance region: the latency-bound phases of small instances overlap.
+  // isorted == null: units of one instance in list order.
+  const int32_t *isorted;
+  const int32_t *icls;
   int64_t n_pairs, pair_offset, Cp;
   const float *params;
   float *X;          // [2][Cp][Dp] NTN inputs (forward)
@@ -331,6 +420,19 @@ __device__ __forceinline__ void csr_row(const CT *__restrict__ col, const float 
   for (; e < e1; ++e) f(col[e], val[e]);
 }
 
+// instance (.x, -1: none) of wave w in unit u of the size-class-sorted list, and the
+// unit size (.y): units of 4 class-0 instances, then of 2 class-1, then single ones
+__device__ __forceinline__ int2 web_unit_q(int u, const int32_t *isorted, int ni, int c1, int c2,
+                                           int U0, int U1, int n_units, int w, int gw) {
+  if (!isorted) return make_int2(u < ni ? u : -1, 1);
+  const bool a0 = u < U0, a1 = !a0 && u < U0 + U1;
+  const int gsz = a0 ? 4 : (a1 ? 2 : 1);
+  const int s0 = a0 ? 4 * u : (a1 ? c1 + 2 * (u - U0) : c2 + (u - U0 - U1));
+  const int end = a0 ? c1 : (a1 ? c2 : ni);
+  const int k = w / (gw / gsz);
+  return make_int2((u < n_units && s0 + k < end) ? isorted[s0 + k] : -1, gsz);
+}
+
 template <bool BWD, int NTB, bool LCSR>
 __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
   using ColT = typename std::conditional<LCSR, uint16_t, int>::type;
@@ -371,37 +473,81 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
   for (int t = 0; t < NTB; ++t) aW0[t][0] = aW0[t][1] = f4{0.f, 0.f, 0.f, 0.f};
   aW1[0] = aW1[1] = f4{0.f, 0.f, 0.f, 0.f};
 
-  // The next instance's inputs are prefetched into registers while this one computes:
+  // ---- unit schedule (GcnArgs::isorted): unit u -> (instances per unit gsz, first
+  // sorted slot, instances present); this thread's instance is number w / (GW_ / gsz)
+  const int64_t n_inst = 2 * A.n_pairs;
+  // (32-bit: a chunk has < 2^31 instances; selects, not branches, so that no table of
+  // the three cases is built in scratch)
+  // (the lambdas below capture locals only: a reference to the kernel argument block
+  // would make the compiler copy it to scratch)
+  const int ni = (int)n_inst;
+  const int32_t *const isorted = A.isorted;
+  const int4 *const ginst = A.inst;
+  const int32_t *const grow_ptr = A.row_ptr, *const gtypes = A.types, *const gcol = A.col;
+  const float *const gval = A.val, *const gGX = A.GX;
+  const int64_t gCp = A.Cp;
+  const int gDp = A.Dp;
+  int c1 = ni, c2 = ni, U0 = 0, U1 = 0, n_units = ni;
+  if (isorted) {
+    c1 = __builtin_amdgcn_readfirstlane(A.icls[1]);
+    c2 = __builtin_amdgcn_readfirstlane(A.icls[2]);
+    U0 = (c1 + 3) >> 2;
+    U1 = (c2 - c1 + 1) >> 1;
+    n_units = U0 + U1 + (ni - c2);
+  }
+  // this thread's instance of unit u (.x, -1: none) and the unit size (.y): a plain
+  // function of values (a lambda's closure got its selects turned into loads from scratch)
+  auto unit_q = [&](int u) __attribute__((always_inline)) -> int2 {
+    return web_unit_q(u, isorted, ni, c1, c2, U0, U1, n_units, w, GW_);
+  };
+
+  // The next unit's inputs are prefetched into registers while this one computes:
   // its (o, N, eb, nnz) at the top of the iteration, its rows after the first phase.
+  // Every thread serves its own instance: node lt = its thread index in the instance's
+  // share of the block (NT / gsz threads).
   constexpr int KM = LCSR ? 4096 / NT : 1;   // CSR entries per thread (LCSR: nnz <= 4096)
   int pr_rp = 0, pr_ty = 0, pr_col[KM];
   float pr_val[KM], pr_gx = 0.f;
-  auto load_rows = [&](int64_t q, int4 in) {
+  auto load_rows = [&](int64_t q, int4 in, int lt) __attribute__((always_inline)) {
     const int o = in.x, N = in.y, eb = in.z, nnz = in.w;
-    pr_rp = tid < N ? A.row_ptr[o + tid] - eb : 0;
-    pr_ty = tid < N ? A.types[o + tid] : 0;
+    pr_rp = lt < N ? grow_ptr[o + lt] - eb : 0;
+    pr_ty = lt < N ? gtypes[o + lt] : 0;
     if (BWD)
-      pr_gx = tid < N ? A.GX[((int64_t)(q & 1) * A.Cp + (q >> 1)) * A.Dp + tid] : 0.f;
+      pr_gx = lt < N ? gGX[((int64_t)(q & 1) * gCp + (q >> 1)) * gDp + lt] : 0.f;
     if (LCSR) {
 #pragma unroll
       for (int k = 0; k < KM; ++k) {
         const int e = tid + k * NT;
-        pr_col[k] = e < nnz ? A.col[eb + e] : 0;
-        pr_val[k] = e < nnz ? A.val[eb + e] : 0.f;
+        pr_col[k] = e < nnz ? gcol[eb + e] : 0;
+        pr_val[k] = e < nnz ? gval[eb + e] : 0.f;
       }
     }
   };
-  const int64_t n_inst = 2 * A.n_pairs;
+  const int2 u0_ = unit_q(blockIdx.x);
+  int64_t q = u0_.x;
+  int gsz = u0_.y;
   int4 in = make_int4(0, 0, 0, 0);
-  if ((int64_t)blockIdx.x < n_inst) {
-    in = A.inst[blockIdx.x];
-    load_rows(blockIdx.x, in);
+  {
+    const int nt_ = NT / gsz, lt_ = tid - (w / (GW_ / gsz)) * nt_;
+    if (q >= 0) {
+      in = ginst[q];
+      load_rows(q, in, lt_);
+    }
   }
-  for (int64_t q = blockIdx.x; q < n_inst; q += gridDim.x) {
-    __syncthreads();   // the previous instance (or the table build) is done with the LDS
-    const int64_t p = q >> 1;
+  for (int unit = blockIdx.x; unit < n_units; unit += gridDim.x) {
+    __syncthreads();   // the previous unit (or the table build) is done with the LDS
+    // this thread's instance of the unit: waves [k WPI, (k+1) WPI), instance region k
+    const int WPI = GW_ / gsz, NTL = NT / gsz;
+    const int kin = w / WPI, lw = w - kin * WPI, lt = tid - kin * NTL;
+    const int cap = (n16max / gsz) & ~15;
+    const int kreg = kin * cap;
+    int *sEtk = sEt + kreg;
+    float *sGxk = sm + L.gx + kreg;
+    float *sZ1k = sZ1 + kreg * ZS;
+    float *sD1k = sD1 + kreg * DS;
+    const int64_t p = q >= 0 ? (q >> 1) : 0;
     const int side = (int)(q & 1);
-    const int o = in.x, N = in.y;
+    const int o = in.x, N = q >= 0 ? in.y : 0;
     const int n16 = (N + 15) & ~15;
     const int ntile = n16 >> 4;
     const uint32_t pk = sg_pair_key(A.key, (uint32_t)(A.pair_offset + p));
@@ -410,10 +556,10 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
     const float *vl;
     // stage the prefetched rows; effective one-hot column per node (sparse dropout of
     // X, layer 0, e = node: d_in = the zero row of sW0 for dropped and absent nodes)
-    if (tid < n16)
-      sEt[tid] = (tid < N && sg_keep(pk, 0, side, tid, A.thr0)) ? pr_ty : d_in;
-    if (BWD && tid < n16) sm[L.gx + tid] = pr_gx;
-    if (LCSR) {
+    if (lt < n16)
+      sEtk[lt] = (lt < N && sg_keep(pk, 0, side, lt, A.thr0)) ? pr_ty : d_in;
+    if (BWD && lt < n16) sGxk[lt] = pr_gx;
+    if (LCSR) {   // units of one instance only (the host passes no isorted with LCSR)
       if (tid < N) sRp[tid] = pr_rp;
       if (tid == 0) sRp[N] = in.w;
 #pragma unroll
@@ -428,14 +574,16 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
     } else {
       rp = A.row_ptr + o; cl = (const ColT *)(const void *)A.col; vl = A.val;
     }
-    const int64_t qn = q + gridDim.x;
-    const int4 inn = qn < n_inst ? A.inst[qn] : make_int4(0, 0, 0, 0);
+    const int2 un_ = unit_q(unit + gridDim.x);
+    const int64_t qn = un_.x;
+    const int gszn = un_.y;
+    const int4 inn = qn >= 0 ? ginst[qn] : make_int4(0, 0, 0, 0);
     __syncthreads();
 
     // ---- forward: H1 (lane (i, g): node 16t+i, features 16c + 4g + s), D1', Z1 ----
 #pragma unroll
     for (int u = 0; u < GCN_TPW; ++u) {
-      const int t = w + u * GW_;
+      const int t = lw + u * WPI;
       if (t >= ntile) break;
       const int n = 16 * t + i;
       float h[8];
@@ -446,7 +594,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
       }
       if (n < N) {
         csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
-          const float *wr = sW0 + sEt[mm] * W0S + 4 * g;
+          const float *wr = sW0 + sEtk[mm] * W0S + 4 * g;
           const float4 wa = *(const float4 *)wr, wb = *(const float4 *)(wr + 16);
           h[0] = fmaf(v, wa.x, h[0]); h[1] = fmaf(v, wa.y, h[1]);
           h[2] = fmaf(v, wa.z, h[2]); h[3] = fmaf(v, wa.w, h[3]);
@@ -471,20 +619,23 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) z = mfma4(h[4 * c + s], sW1[(16 * c + 4 * g + s) * WH2 + i], z);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sZ1[(16 * t + 4 * g + r) * ZS + i] = z[r];
+      for (int r = 0; r < 4; ++r) sZ1k[(16 * t + 4 * g + r) * ZS + i] = z[r];
       if (BWD) {
-        *(float4 *)(sD1 + n * DS + 4 * g) = make_float4(h[0], h[1], h[2], h[3]);
-        *(float4 *)(sD1 + n * DS + 16 + 4 * g) = make_float4(h[4], h[5], h[6], h[7]);
+        *(float4 *)(sD1k + n * DS + 4 * g) = make_float4(h[0], h[1], h[2], h[3]);
+        *(float4 *)(sD1k + n * DS + 16 + 4 * g) = make_float4(h[4], h[5], h[6], h[7]);
       }
     }
     __syncthreads();
-    if (qn < n_inst) load_rows(qn, inn);   // lands during the rest of this instance
+    if (qn >= 0) {   // lands during the rest of this unit
+      const int ntn = NT / gszn;
+      load_rows(qn, inn, tid - (w / (GW_ / gszn)) * ntn);
+    }
 
     // ---- H2 (lane (i, g): node 16t+i, features 4g..4g+3), Dense, Padding, NTN input ----
     float gzr[GCN_TPW][4];
 #pragma unroll
     for (int u = 0; u < GCN_TPW; ++u) {
-      const int t = w + u * GW_;
+      const int t = lw + u * WPI;
       if (t >= ntile) break;
       const int n = 16 * t + i;
       float h2[4] = {0.f, 0.f, 0.f, 0.f};
@@ -492,7 +643,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
         const float4 b = *(const float4 *)(sb1 + 4 * g);
         h2[0] = b.x; h2[1] = b.y; h2[2] = b.z; h2[3] = b.w;
         csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
-          const float4 zz = *(const float4 *)(sZ1 + mm * ZS + 4 * g);
+          const float4 zz = *(const float4 *)(sZ1k + mm * ZS + 4 * g);
           h2[0] = fmaf(v, zz.x, h2[0]); h2[1] = fmaf(v, zz.y, h2[1]);
           h2[2] = fmaf(v, zz.z, h2[2]); h2[3] = fmaf(v, zz.w, h2[3]);
         });
@@ -512,7 +663,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
           A.X[((int64_t)side * A.Cp + p) * A.Dp + n] = k4 ? z * A.ik4 : 0.f;
       } else {
         // Dense / Padding / NTN-input backward: gZ1 (= gH2, identity act) in registers
-        const float gx = k4 ? sm[L.gx + n] * A.ik4 : 0.f;
+        const float gx = k4 ? sGxk[n] * A.ik4 : 0.f;
         const float gp = (n < N && pre > 0.f) ? gx : 0.f;
         if (g == 0) aBd += gp;
 #pragma unroll
@@ -525,19 +676,22 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
     }
     if (!BWD) {
       // Padding rows [N, Dp): padding_value (zero beyond D), after the NTN-input dropout
-      for (int a = N + tid; a < A.Dp; a += NT)
-        A.X[((int64_t)side * A.Cp + p) * A.Dp + a] =
-            (a < A.D && A.padv != 0.f && sg_keep(pk, 4, side, (uint32_t)a, A.thr4))
-                ? A.padv * A.ik4 : 0.f;
+      if (q >= 0)
+        for (int a = N + lt; a < A.Dp; a += NTL)
+          A.X[((int64_t)side * A.Cp + p) * A.Dp + a] =
+              (a < A.D && A.padv != 0.f && sg_keep(pk, 4, side, (uint32_t)a, A.thr4))
+                  ? A.padv * A.ik4 : 0.f;
       in = inn;
+      q = qn;
+      gsz = gszn;
       continue;
     }
     __syncthreads();   // every wave is done reading Z1: it becomes gZ1
 #pragma unroll
     for (int u = 0; u < GCN_TPW; ++u) {
-      const int t = w + u * GW_;
+      const int t = lw + u * WPI;
       if (t >= ntile) break;
-      *(float4 *)(sZ1 + (16 * t + i) * ZS + 4 * g) =
+      *(float4 *)(sZ1k + (16 * t + i) * ZS + 4 * g) =
           make_float4(gzr[u][0], gzr[u][1], gzr[u][2], gzr[u][3]);
     }
     __syncthreads();
@@ -545,13 +699,13 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
     // ---- gS1 = Â·gZ1 (lane (i, g): node 16t+i, j = 4g..4g+3); gD1 = gS1·W1ᵀ; gW1 ----
 #pragma unroll
     for (int u = 0; u < GCN_TPW; ++u) {
-      const int t = w + u * GW_;
+      const int t = lw + u * WPI;
       if (t >= ntile) break;
       const int n = 16 * t + i;
       float q4[4] = {0.f, 0.f, 0.f, 0.f};
       if (n < N)
         csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
-          const float4 gg = *(const float4 *)(sZ1 + mm * ZS + 4 * g);
+          const float4 gg = *(const float4 *)(sZ1k + mm * ZS + 4 * g);
           q4[0] = fmaf(v, gg.x, q4[0]); q4[1] = fmaf(v, gg.y, q4[1]);
           q4[2] = fmaf(v, gg.z, q4[2]); q4[3] = fmaf(v, gg.w, q4[3]);
         });
@@ -569,7 +723,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
         const int nn = 16 * t + 4 * g + s;
         const float b = scr[(4 * g + s) * WH2 + i];
 #pragma unroll
-        for (int cb = 0; cb < 2; ++cb) aW1[cb] = mfma4(sD1[nn * DS + 16 * cb + i], b, aW1[cb]);
+        for (int cb = 0; cb < 2; ++cb) aW1[cb] = mfma4(sD1k[nn * DS + 16 * cb + i], b, aW1[cb]);
       }
       sg_wsync();
       // gP0 = relu'·keep·gD1·ik1 = (D1' > 0) · gD1·ik1, in place of D1'
@@ -577,7 +731,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
       for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float *dp = sD1 + (16 * t + 4 * g + r) * DS + 16 * cb + i;
+          float *dp = sD1k + (16 * t + 4 * g + r) * DS + 16 * cb + i;
           const float v = *dp > 0.f ? gd[cb][r] : 0.f;
           aB0[cb] += v;
           *dp = v;
@@ -588,7 +742,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
     // ---- gS0 = Â·gP0 (rows n = 16t + 4g + s, features i, 16 + i); gW0 += Xᵀ·(scale0·gS0) ----
 #pragma unroll
     for (int u = 0; u < GCN_TPW; ++u) {
-      const int t = w + u * GW_;
+      const int t = lw + u * WPI;
       if (t >= ntile) break;
       float bq[4][2];
       int et[4];
@@ -596,11 +750,11 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
       for (int s = 0; s < 4; ++s) {
         const int n = 16 * t + 4 * g + s;
         float q0 = 0.f, q1 = 0.f;
-        et[s] = sEt[n];
+        et[s] = sEtk[n];
         if (n < N && et[s] < d_in)
           csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
-            q0 = fmaf(v, sD1[mm * DS + i], q0);
-            q1 = fmaf(v, sD1[mm * DS + 16 + i], q1);
+            q0 = fmaf(v, sD1k[mm * DS + i], q0);
+            q1 = fmaf(v, sD1k[mm * DS + 16 + i], q1);
           });
         bq[s][0] = q0 * A.ik0;   // scale0 = keep0 · ik0 (dropped nodes: et = d_in, q = 0)
         bq[s][1] = q1 * A.ik0;
@@ -615,6 +769,8 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
         }
     }
     in = inn;
+    q = qn;
+    gsz = gszn;
   }
   if (!BWD) return;
   __syncthreads();
@@ -1626,6 +1782,8 @@ static int gcn_launch(bool bwd, const WebPlan &W, const GcnArgs &A, int64_t n_in
                     A.max_nnz <= 4096;
   const size_t lds = gcn_lds_bytes(W, A.n_max, A.max_nnz, bwd, lcsr);
   if (lds > 163840u) return SG_ERR_UNSUPPORTED;
+  GcnArgs A_ = A;
+  if (lcsr) A_.isorted = nullptr, A_.icls = nullptr;   // LCSR stages one instance at a time
   int per_cu = (int)(163840u / lds);
   if (per_cu > 2048 / (64 * gcn_gw(bwd))) per_cu = 2048 / (64 * gcn_gw(bwd));
   int64_t blocks = (int64_t)sg_num_cus() * per_cu;
@@ -1637,7 +1795,7 @@ static int gcn_launch(bool bwd, const WebPlan &W, const GcnArgs &A, int64_t n_in
     const void *fn = (const void *)web_gcn_kernel<B, NT, LC>;                                 \
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);      \
     hipLaunchKernelGGL((web_gcn_kernel<B, NT, LC>), dim3((unsigned)blocks), dim3(64 * gcn_gw(B)), \
-                       lds, st, A);                                                           \
+                       lds, st, A_);                                                          \
   } while (0)
 #define SG_WEB_GCN_NT(NT)                             \
   do {                                                \
@@ -1730,6 +1888,11 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
   H.inv_batch = batch_total > 0 ? 1.f / (float)batch_total : 0.f;
   const size_t head_lds = (size_t)K * 2 * Dp * 4u;
   const int full = W.padv != 0.f ? 1 : 0;
+  // instance units (GcnArgs::isorted); SG_WEB_UNITS=0 runs one instance per workgroup
+  static const bool units = [] {
+    const char *e = getenv("SG_WEB_UNITS");
+    return !(e && e[0] == '0');
+  }();
 
   for (int64_t c0 = 0; c0 < n_pairs; c0 += chunk) {
     const int64_t n = n_pairs - c0 < chunk ? n_pairs - c0 : chunk;
@@ -1739,6 +1902,22 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
                        store->node_off, store->row_ptr, full, D, EXT, EXT16, EXT128, INST);
     G.pairs = pc;
     G.inst = INST;
+    G.isorted = nullptr;
+    G.icls = nullptr;
+    if (units) {   // instance units: small instances share a workgroup (web_gcn_kernel)
+      const int n16 = (store->n_max + 15) & ~15;
+      const int cap4 = (n16 / 4) & ~15, cap2 = (n16 / 2) & ~15;
+      const int nbu = (int)((2 * n + kUnitChunk - 1) / kUnitChunk);
+      int32_t *isort = (int32_t *)(base + ws.ISORT), *icnt = (int32_t *)(base + ws.ICNT);
+      int32_t *icls = (int32_t *)(base + ws.ICLS);
+      hipLaunchKernelGGL(web_icls_count, dim3(nbu), dim3(256), 0, st, INST, 2 * n, cap4, cap2,
+                         nbu, icnt);
+      hipLaunchKernelGGL(web_icls_scan, dim3(1), dim3(64), 0, st, icnt, nbu, 2 * n, icls);
+      hipLaunchKernelGGL(web_icls_scatter, dim3(nbu), dim3(256), 0, st, INST, 2 * n, cap4, cap2,
+                         nbu, (const int32_t *)icnt, isort);
+      G.isorted = isort;
+      G.icls = icls;
+    }
     G.n_pairs = n;
     G.pair_offset = pair_offset + c0;
     if ((rc = gcn_launch(false, W, G, 2 * n, st)) != SG_OK) return rc;
