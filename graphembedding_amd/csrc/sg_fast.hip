@@ -255,6 +255,8 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   const int d_in = A.d_in;
   const float *__restrict__ prm = A.params;
   uint32_t key = A.key;   // sg_seed_key of the dropout seed
+  const uint32_t thr0s = __builtin_amdgcn_readfirstlane(A.thr0);
+  const uint32_t thr4s = __builtin_amdgcn_readfirstlane(A.thr4);
   if (A.seed_dev) {
     const uint64_t sd = *A.seed_dev;
     key = ((uint32_t)sd * 0x85EBCA6Bu) ^ (uint32_t)(sd >> 32);
@@ -589,7 +591,10 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       const int e = l & 15;
       const bool hi = l >= 16;
       const uint32_t h = sg_hash(pk, hi ? NL : 0u, (uint32_t)e);
-      const uint32_t thr = hi ? A.thr4 : A.thr0;
+      // both thresholds as scalar values first: a select between two kernel-argument
+      // fields compiled to a per-lane load from the argument block inside the pair loop
+      // (global_load + s_waitcnt vmcnt(0), which also waited for the next record's prefetch)
+      const uint32_t thr = hi ? thr4s : thr0s;
       // node presence folds into the node mask, and into the NTN mask when the NTN
       // input is indexed by node (Padding); after Average it is indexed by feature
       const bool p0 = (hi && AVG) || e < N0, p1 = (hi && AVG) || e < N1;

@@ -150,6 +150,8 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
   const uint32_t lb2 = (uint32_t)(FH2 * g + j);   // layer 2: e = 16 n + j
   const int d_in = A.d_in, D = A.D;
   const float *__restrict__ prm = A.params;
+  const uint32_t thr0s = __builtin_amdgcn_readfirstlane(A.thr0);
+  const uint32_t thr4s = __builtin_amdgcn_readfirstlane(A.thr4);
 
   // ---- parameter staging (behind the shared tables) and tables ----
   float *sW0 = smem;                            // W0 · ik0 · ik1, row d_in zero
@@ -380,7 +382,10 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
       const int e = l & 31;
       const bool hi = l >= 32;
       const uint32_t h = sg_hash(pk, hi ? 4u : 0u, (uint32_t)e);
-      const uint32_t thr = hi ? A.thr4 : A.thr0;
+      // both thresholds as scalar values first: a select between two kernel-argument
+      // fields compiled to a per-lane load from the argument block inside the pair loop
+      // (global_load + s_waitcnt vmcnt(0), which also waited for the next record's prefetch)
+      const uint32_t thr = hi ? thr4s : thr0s;
       const uint64_t b0 = __ballot((e < N0) & ((h & 0xFFFFu) < thr));
       const uint64_t b1 = __ballot((e < N1) & ((h >> 16) < thr));
       km0[0] = (uint32_t)b0;

@@ -46,7 +46,9 @@ def test_fused_store_source_matches_records(gpu, stack):
     for b in (b_list, b_grid):
         for x, y in zip(ref, run(b)):
             assert torch.equal(x, y)
-    model.balance(b_rec)
+    # the store-sourced path walks the order with the mixed schedule (no class table),
+    # so the record batch does too for a bitwise comparison
+    model.balance(b_rec, classes=False)
     model.balance(b_grid)
     assert torch.equal(b_rec.order, b_grid.order)
     for x, y in zip(run(b_rec), run(b_grid)):
