@@ -159,7 +159,10 @@ template <int D, bool AVG = false>
 struct FastLds {
   // NTN width DN (the Padding width D, or H2's 16 features after Average), the row
   // stride WR of the NTN W tables and VS of the V table
-  static constexpr int DN = AVG ? FH2 : D, WR = AVG ? 16 : 12, VS = AVG ? 32 : 24;
+  // VS = 34 (≡ 2 mod 32): the V reads sV[kc·VS + a] of lanes (g, kc) hit distinct banks
+  // (2 kc + g); a stride of 24 or 32 put three or ten rows kc on one bank
+  static constexpr int DN = AVG ? FH2 : D, WR = AVG ? 16 : 12, VS = 34;
+  static_assert(2 * DN <= VS, "V row");
   static constexpr int RW = 2 * D * D + 2 * D + 4;  // record words (multiple of 4)
   static constexpr int REC = 0;
   static constexpr int TILE = REC + RW;               // 2 x 16 x TS1 (D1 tiles)

@@ -47,9 +47,23 @@ constexpr uint32_t WA_SWZ0 = 0x2ccb8ff2u, WA_SWZ1 = 0x17a0853u;
 __device__ __forceinline__ int wa_swz(int k, int a) {
   return (int)(((a & 1) ? WA_SWZ1 : WA_SWZ0) >> (3 * k)) & 7;
 }
-constexpr int VS = 64;     // V[k][c] row stride (c < 2D)
+// V[k][c] row stride (c < 2D): 66 ≡ 2 mod 32, so the reads sV[kc·VS + a] of lanes (g, kc)
+// hit distinct banks (2 kc + g); at 64 the ten rows kc shared one bank (10-way conflicts)
+constexpr int VS = 66;
 constexpr int NBUF = 80;   // NTN buffer floats per pair: x1[32] | x2[32] | gm[16]
 constexpr int MAXW = 8;    // waves per block (2 per SIMD)
+#ifndef SG32_HOIST_P1
+#define SG32_HOIST_P1 1
+#endif
+#ifndef SG32_AF_ALL
+#define SG32_AF_ALL 1
+#endif
+#ifndef SG32_NTN_KR
+#define SG32_NTN_KR 1
+#endif
+#ifndef SG32_V_HOIST
+#define SG32_V_HOIST 0
+#endif
 
 
 struct F32Args {
@@ -279,6 +293,20 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
     }
     const int p = pnext;
     // ---- stage the record (f32 LDS image; bf16 Â widened) ----
+#ifdef SG32_ABL_NOREC   // timing ablation only (results invalid): every pair reuses the first
+                        // record's Â and types with its own node counts (store source only)
+    if (it > 0 && A.src_store && A.sn != nullptr) {
+      int g0, g1;
+      f32_pair_ids(A, p, g0, g1);
+      const int n0 = A.sn[g0], n1 = A.sn[g1];
+      sg_wsync();
+      if (l == 0) {
+        ((int *)sRec)[L::TAIL + 2 * NC] = n0;
+        ((int *)sRec)[L::TAIL + 2 * NC + 1] = n1;
+      }
+      sg_wsync();
+    } else
+#endif
     {
       constexpr int NREC = (RW4 + 63) / 64;
       uint4 v[NREC];
@@ -400,8 +428,15 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
         const int ab = abase0 + s * NC * RS + 4 * b;
+        // unconditional: entries past N are zero (record contract), and reads without a
+        // per-k-block branch issue together (one LDS round trip instead of one per block)
+#if SG32_AF_ALL
+        af[0][b] = W[ab];
+        af[1][b] = W[ab + 16 * RS];
+#else
         af[0][b] = b < KB ? W[ab] : 0.f;
         af[1][b] = (b < KB && T > 1) ? W[ab + 16 * RS] : 0.f;
+#endif
       }
     };
 
@@ -418,6 +453,51 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
         d1[s][to][0] = f4{b0v0, b0v0, b0v0, b0v0};
         d1[s][to][1] = f4{b0v1, b0v1, b0v1, b0v1};
       }
+#if SG32_HOIST_P1
+      // types, W0 rows and Â fragments of all eight k-blocks first (unconditional reads,
+      // two dependent LDS round trips per side instead of two per k-block): nodes past N
+      // are masked (k0 = 0 -> the zero row d_in), Â is zero there
+      uint32_t t8[8];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) t8[b] = (uint32_t)ty[s * NC + 4 * b + g];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const uint32_t t_ = min(t8[b], (uint32_t)(d_in - 1));
+        const uint32_t k0 = (kms >> (4 * b + g)) & 1u;
+        t8[b] = k0 ? t_ : 63u;   // 63: dropped / absent (the W0 row read is d_in's zero row)
+        tp[b >> 2] |= t8[b] << (6 * (b & 3));
+      }
+      // two halves of four k-blocks (the second only for sides of more than 16 nodes):
+      // the reads of a half issue together
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb) {
+        if (hb == 0 || KB > 4) {
+          float z0a[4], z0b[4], a0v[4], a1v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int b = 4 * hb + i;
+            const float *w0 = sW0 + (t8[b] == 63u ? (uint32_t)d_in : t8[b]) * FH1 + j;
+            z0a[i] = w0[0];
+            z0b[i] = w0[16];
+            const int ab = abase0 + s * NC * RS + 4 * b;
+            a0v[i] = W[ab];
+            a1v[i] = W[ab + 16 * RS];
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int b = 4 * hb + i;
+            if (b < KB) {
+              d1[s][0][0] = mfma4(a0v[i], z0a[i], d1[s][0][0]);
+              d1[s][0][1] = mfma4(a0v[i], z0b[i], d1[s][0][1]);
+              if (T > 1) {
+                d1[s][1][0] = mfma4(a1v[i], z0a[i], d1[s][1][0]);
+                d1[s][1][1] = mfma4(a1v[i], z0b[i], d1[s][1][1]);
+              }
+            }
+          }
+        }
+      }
+#else
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
         if (b < KB) {
@@ -441,6 +521,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
           tp[b >> 2] |= 63u << (6 * (b & 3));
         }
       }
+#endif
       tyA[s][0] = tp[0];
       tyA[s][1] = tp[1];
     }
@@ -554,36 +635,73 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
     float u[8], cs[8];
 #pragma unroll
     for (int rr = 0; rr < 8; ++rr) u[rr] = cs[rr] = 0.f;
+#ifdef SG32_ABL_NONTN   // timing ablation only (results invalid): no NTN W products
+    constexpr int NTN_BQ = 0;
+#else
+    constexpr int NTN_BQ = 8;
+#endif
+    // The Wa rows of one column block are read together (one LDS round trip per block):
+    // KR rows, KB0 rounded up to even, as straight-line code per KR.  Rows KB0..KR-1 of
+    // x1 are zero, so their u rows go unused and their cb terms are exact fmaf(0, w, cb).
+    auto ntn_fwd = [&](auto KRc) __attribute__((always_inline)) {
+      constexpr int KR = decltype(KRc)::value;
 #pragma unroll
-    for (int bq = 0; bq < 8; ++bq) {
-      if (bq < KB1) {
-        const f4 x2 = *(const f4 *)(sX + NC + 4 * bq);
-        float cb[4] = {0.f, 0.f, 0.f, 0.f};
-        const float *wb = sWa + walane + ((4 * bq) ^ wswz);
+      for (int bq = 0; bq < NTN_BQ; ++bq) {
+        if (bq < KB1) {
+          const f4 x2 = *(const f4 *)(sX + NC + 4 * bq);
+          const float *wb = sWa + walane + ((4 * bq) ^ wswz);
+          f4 w[KR];
 #pragma unroll
-        for (int rr = 0; rr < 8; ++rr) {
-          if (rr < KB0) {
-            const f4 w = *(const f4 *)(wb + rr * 4 * FK * WAS);   // rows a >= D are zero
+          for (int rr = 0; rr < KR; ++rr) w[rr] = *(const f4 *)(wb + rr * 4 * FK * WAS);   // rows a >= D are zero
+          float cb[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int rr = 0; rr < KR; ++rr) {
             const float x1a = xo[0][rr];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              u[rr] = fmaf(w[e], x2[e], u[rr]);
-              cb[e] = fmaf(x1a, w[e], cb[e]);
+              u[rr] = fmaf(w[rr][e], x2[e], u[rr]);
+              cb[e] = fmaf(x1a, w[rr][e], cb[e]);
             }
           }
-        }
-        float hs[2];
+          float hs[2];
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(cb[e]),
-                                                            __float_as_uint(cb[e + 2]), false, false);
-          hs[e] = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+          for (int e = 0; e < 2; ++e) {
+            const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(cb[e]),
+                                                              __float_as_uint(cb[e + 2]), false, false);
+            hs[e] = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+          }
+          const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(hs[0]),
+                                                            __float_as_uint(hs[1]), false, false);
+          cs[bq] = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
         }
-        const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(hs[0]),
-                                                          __float_as_uint(hs[1]), false, false);
-        cs[bq] = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
       }
+    };
+#if SG32_NTN_KR
+    if (KB0 > 6) ntn_fwd(std::integral_constant<int, 8>{});
+    else if (KB0 > 4) ntn_fwd(std::integral_constant<int, 6>{});
+    else if (KB0 > 2) ntn_fwd(std::integral_constant<int, 4>{});
+    else ntn_fwd(std::integral_constant<int, 2>{});
+#else
+    ntn_fwd(std::integral_constant<int, 8>{});   // (KR = 8: every row read)
+#endif
+#if SG32_V_HOIST >= 1
+    // V entries of the lane's rows, read unconditionally (one LDS round trip; rows past
+    // the sides' k-blocks are never used): vu = u + V[k][a] (forward and ∂L/∂x1)
+    float vu[8], vb[8];
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      const int a = 4 * rr + g;
+      const int ac = a < D ? a : 0;
+      vu[rr] = u[rr] + sV[kc * VS + ac];
+      vb[rr] = sV[kc * VS + D + ac];
     }
+    float mpart = 0.f;
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      if (rr < KB0) mpart = fmaf(xo[0][rr], vu[rr], mpart);
+      if (rr < KB1) mpart = fmaf(xo[1][rr], vb[rr], mpart);
+    }
+#else
     float mpart = 0.f;
 #pragma unroll
     for (int rr = 0; rr < 8; ++rr) {
@@ -598,6 +716,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
         mpart = fmaf(xo[1][rr], sV[kc * VS + D + bc], mpart);
       }
     }
+#endif
     const float m = xsum32(xsum16(mpart)) + bnk;
     const float rk = (kv & (m > 0.f)) ? m : 0.f;
     const float rsum = row_sum16(rk);
@@ -629,22 +748,39 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
       if (g == 0) nb_[2 * NC + j] = gmk;
     }
     const float gmk4 = gmk * A.ik4;
+#if SG32_V_HOIST >= 2
+    // the V entries of side 1's rows read unconditionally (one LDS round trip)
+    float vb2[8];
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      const int b = 4 * rr + g;
+      vb2[rr] = sV[kc * VS + D + (b < D ? b : 0)];
+    }
+#endif
     float ge[2][8];   // dL/dx · ik4 (before the x > 0 mask) of the lane's rows
 #pragma unroll
     for (int rr = 0; rr < 8; ++rr) {
       ge[0][rr] = ge[1][rr] = 0.f;
       if (rr < KB0) {
+#if SG32_V_HOIST >= 1
+        ge[0][rr] = row_sum16(gmk4 * vu[rr]);
+#else
         const int a = 4 * rr + g;
         const int ac = a < D ? a : 0;
         ge[0][rr] = row_sum16(gmk4 * (sV[kc * VS + ac] + u[rr]));
+#endif
       }
     }
 #pragma unroll
     for (int rr = 0; rr < 8; ++rr) {
       if (rr < KB1) {
+#if SG32_V_HOIST >= 2
+        ge[1][rr] = row_sum16(gmk4 * (vb2[rr] + cs[rr]));
+#else
         const int b = 4 * rr + g;
         const int bc = b < D ? b : 0;
         ge[1][rr] = row_sum16(gmk4 * (sV[kc * VS + D + bc] + cs[rr]));
+#endif
       }
     }
 
