@@ -133,14 +133,21 @@ int web_plan(const sg_model_t *m, WebPlan *W) {
 // ---------------------------------------------------------------------------
 struct WebWs {
   int64_t Cp;                                        // chunk rounded up to TB
-  int64_t X, GX, T, GM, EXT, EXT16, EXT128, INST;    // per-chunk buffers
+  // per-chunk buffers, one set per pipeline slot (slot 1 = slot 0 + SLOT): the
+  // instance kernels of chunk c + 1 overlap the NTN GEMMs of chunk c (sg_web_run)
+  int64_t X, GX, T, GM, EXT, EXT16, EXT128, INST;
   int64_t ISORT, ICNT, ICLS;                         // instance units (web_icls_*)
+  int64_t SLOT;                                      // floats per slot
   int64_t Wg, Wh, GWS, GVS, GSLAB, HSLABo, total;    // per-call buffers
   int gcn_blocks, head_blocks;
 };
 
 int gcn_blocks_for() { return sg_num_cus(); }
 int head_blocks_for() { return 2 * sg_num_cus(); }
+
+#ifndef SG_WEB_T_BF3
+#define SG_WEB_T_BF3 1
+#endif
 
 WebWs web_ws(const WebPlan &W, int64_t chunk) {
   WebWs w;
@@ -151,7 +158,8 @@ WebWs web_ws(const WebPlan &W, int64_t chunk) {
   auto take = [&](int64_t n) { const int64_t r = o; o += (n + 63) & ~(int64_t)63; return r; };
   w.X = take(2 * w.Cp * Dp);        // X1 | X2
   w.GX = take(2 * w.Cp * Dp);       // gX1 | gX2
-  w.T = take(w.Cp * K * Dp);
+  // T: the a-tile shares MP[p][k][4] of web_t_kernel_b3<true>, or all of T (f32 path)
+  w.T = take(SG_WEB_T_BF3 ? w.Cp * WKP * 4 : w.Cp * K * Dp);
   w.GM = take(w.Cp * WKP);
   w.EXT = take(2 * w.Cp);           // int2 per pair
   w.EXT16 = take(2 * (w.Cp / 16));
@@ -160,6 +168,8 @@ WebWs web_ws(const WebPlan &W, int64_t chunk) {
   w.ISORT = take(2 * w.Cp);         // instances sorted by size class
   w.ICNT = take(3 * ((2 * w.Cp + kUnitChunk - 1) / kUnitChunk));
   w.ICLS = take(4);
+  w.SLOT = o;
+  o += w.SLOT;                      // slot 1
   w.Wg = take(K * Dp * Dp);
   w.Wh = take(K * Dp * Dp);
   w.GWS = take((int64_t)WSPLIT * K * Dp * Dp);
@@ -332,14 +342,19 @@ __global__ void __launch_bounds__(256) web_wprep_h(const float *__restrict__ Wg,
 // t % waves (N <= 512: 32 tiles).  The sparse loops read the instance's CSR rows
 // through the caches; LCSR (opt-in) stages them in LDS first.
 // ---------------------------------------------------------------------------
-// waves per instance workgroup: 16 forward (2 tiles per wave), SG_WEB_BWD_WAVES backward.
+// waves per instance workgroup: SG_WEB_FWD_WAVES forward, SG_WEB_BWD_WAVES backward.
 // The backward wants more than the 128 VGPRs of a 16-wave block and spills ~32 of them
 // there, but twice the waves per instance hide the latency-bound sparse phases better:
 // 16 waves measured 411 -> 379 ms per C5 step against 8 (246 VGPRs, no spills).
 #ifndef SG_WEB_BWD_WAVES
 #define SG_WEB_BWD_WAVES 16
 #endif
-__host__ __device__ constexpr int gcn_gw(bool bwd) { return bwd ? SG_WEB_BWD_WAVES : 16; }
+// forward instance kernel: 8 waves (4 tiles each) measured 3.596 vs 3.571 M pairs/s
+// against 16 on C5 (one stream), 3.610 with the chunk pipeline (profiles/r03_c5fw8/)
+#ifndef SG_WEB_FWD_WAVES
+#define SG_WEB_FWD_WAVES 8
+#endif
+__host__ __device__ constexpr int gcn_gw(bool bwd) { return bwd ? SG_WEB_BWD_WAVES : SG_WEB_FWD_WAVES; }
 
 struct GcnArgs {
   const int32_t *node_off, *types, *row_ptr, *col;
@@ -934,9 +949,6 @@ __global__ void __launch_bounds__(256) web_t_kernel(const float *__restrict__ X2
 // LDS: [part][128 rows][40 bf16] per operand (80-byte rows: the b128 fragment reads
 // of 8 consecutive rows fall on distinct banks), 60 KiB; 32-deep contraction chunks,
 // the next chunk's f32 operands prefetched into registers during the MFMAs.
-#ifndef SG_WEB_T_BF3
-#define SG_WEB_T_BF3 1
-#endif
 constexpr int B3K = 32, B3S = 40;   // contraction chunk, LDS row stride (bf16)
 constexpr int B3PART = TB * B3S;    // bf16 per part plane
 
@@ -1786,6 +1798,10 @@ static int gcn_launch(bool bwd, const WebPlan &W, const GcnArgs &A, int64_t n_in
   if (lcsr) A_.isorted = nullptr, A_.icls = nullptr;   // LCSR stages one instance at a time
   int per_cu = (int)(163840u / lds);
   if (per_cu > 2048 / (64 * gcn_gw(bwd))) per_cu = 2048 / (64 * gcn_gw(bwd));
+  if (!bwd) {   // A/B: forward blocks per CU (room for the pipelined GEMMs beside them)
+    const char *e = getenv("SG_WEB_FWD_BPC");
+    if (e && atoi(e) > 0 && atoi(e) < per_cu) per_cu = atoi(e);
+  }
   int64_t blocks = (int64_t)sg_num_cus() * per_cu;
   if (bwd) blocks = sg_num_cus();   // one slab row per block (web_ws sizes the slab for this)
   if (blocks > n_inst) blocks = n_inst;
@@ -1824,6 +1840,29 @@ int sg_web_lds_ok(const sg_model_t *m) {
   return gcn_lds_bytes(W, m->n_max, 0, true, false) <= 163840u;
 }
 
+// The chunk pipeline's second stream and its events (sg_web_run: F = a chunk's forward
+// instance kernel done, G[slot] = the GEMMs of the chunk in that workspace slot done),
+// created once per host thread and device
+static int web_aux(hipStream_t *gs, hipEvent_t *evF, hipEvent_t *evG) {
+  constexpr int kMaxDev = 64;
+  thread_local hipStream_t streams[kMaxDev] = {};
+  thread_local hipEvent_t evs[kMaxDev][3] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return SG_ERR_HIP;
+  if (!streams[dev]) {
+    for (int e = 0; e < 3; ++e)
+      if (hipEventCreateWithFlags(&evs[dev][e], hipEventDisableTiming) != hipSuccess)
+        return SG_ERR_HIP;
+    if (hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess)
+      return SG_ERR_HIP;
+  }
+  *gs = streams[dev];
+  *evF = evs[dev][0];
+  evG[0] = evs[dev][1];
+  evG[1] = evs[dev][2];
+  return SG_OK;
+}
+
 int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *pairs,
                const float *labels, int64_t n_pairs, int64_t pair_offset, int64_t batch_total,
                const float *params, uint64_t seed, const float *y_stats, int add_label,
@@ -1840,10 +1879,6 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
   (void)hipGetLastError();   // report only this call's launch errors
   const WebWs ws = web_ws(W, chunk);
   float *base = (float *)workspace;
-  float *X = base + ws.X, *GX = base + ws.GX, *T = base + ws.T, *GM = base + ws.GM;
-  int2 *EXT = (int2 *)(base + ws.EXT), *EXT16 = (int2 *)(base + ws.EXT16);
-  int2 *EXT128 = (int2 *)(base + ws.EXT128);
-  int4 *INST = (int4 *)(base + ws.INST);
   float *Wg = base + ws.Wg, *Wh = base + ws.Wh, *GWS = base + ws.GWS, *GVS = base + ws.GVS;
   float *GSLAB = base + ws.GSLAB, *HS = base + ws.HSLABo;
   const int Dp = W.Dp, K = W.K, D = W.D;
@@ -1869,8 +1904,6 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
   G.val = store->val;
   G.Cp = ws.Cp;
   G.params = params;
-  G.X = X;
-  G.GX = GX;
   G.slab = GSLAB;
   G.key = sg_seed_key(seed);
   G.thr0 = W.thr0; G.thr1 = W.thr1; G.thr2 = W.thr2; G.thr4 = W.thr4;
@@ -1880,8 +1913,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
   G.max_nnz = store->max_nnz;
   G.ob0 = W.ob0; G.oW1 = W.oW1; G.ob1 = W.ob1; G.oWd = W.oWd; G.obd = W.obd;
   HeadArgs H;
-  H.X = X; H.T = T; H.params = params; H.labels = labels; H.y_stats = y_stats;
-  H.ext = EXT; H.ext128 = EXT128; H.GX = GX; H.GM = GM; H.s_out = nullptr; H.hslab = HS;
+  H.params = params; H.y_stats = y_stats; H.s_out = nullptr; H.hslab = HS;
   H.Cp = ws.Cp; H.D = D; H.Dp = Dp; H.K = K; H.oV = W.oV; H.oU = W.oU; H.obn = W.obn;
   H.final_act = W.final_act; H.loss_mode = W.loss_mode; H.ntn_mode = W.ntn_mode;
   H.yeta = W.yeta;
@@ -1894,71 +1926,138 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     return !(e && e[0] == '0');
   }();
 
-  for (int64_t c0 = 0; c0 < n_pairs; c0 += chunk) {
-    const int64_t n = n_pairs - c0 < chunk ? n_pairs - c0 : chunk;
+  // Two-stream pipeline over the chunks.  The instance kernels are latency-bound (most
+  // wave cycles wait on the CSR gathers) and the NTN GEMMs are MFMA work, so the forward
+  // instance kernel of chunk c + 1 (stream st) runs while the GEMMs and the head of chunk
+  // c run on a second stream (gs); the backward instance kernel of chunk c then waits
+  // for them.  Per-chunk buffers alternate between two slots.  Every accumulation keeps
+  // its order (GWS/GVS/HS on gs, GSLAB on st, chunks in order), so results are bitwise
+  // those of the one-stream sequence (SG_WEB_PIPE=0).
+  const char *pipe_e = getenv("SG_WEB_PIPE");   // read per call (a test toggles it)
+  const bool pipe_env = !(pipe_e && pipe_e[0] == '0');
+  hipStream_t gs = st;
+  hipEvent_t evF = nullptr, evG[2] = {nullptr, nullptr};
+  const int64_t nch = n_pairs > 0 ? (n_pairs + chunk - 1) / chunk : 0;
+  if (pipe_env && nch > 1) {
+    if (web_aux(&gs, &evF, evG) != SG_OK) return SG_ERR_HIP;
+  }
+  const bool pipe = gs != st;
+  struct Slot {
+    float *X, *GX, *T, *GM;
+    int2 *EXT, *EXT16, *EXT128;
+    int4 *INST;
+    int32_t *isort, *icnt, *icls;
+  };
+  auto slot = [&](int64_t c) {
+    float *sb = base + (pipe ? (c & 1) * ws.SLOT : 0);
+    Slot S;
+    S.X = sb + ws.X; S.GX = sb + ws.GX; S.T = sb + ws.T; S.GM = sb + ws.GM;
+    S.EXT = (int2 *)(sb + ws.EXT); S.EXT16 = (int2 *)(sb + ws.EXT16);
+    S.EXT128 = (int2 *)(sb + ws.EXT128); S.INST = (int4 *)(sb + ws.INST);
+    S.isort = (int32_t *)(sb + ws.ISORT); S.icnt = (int32_t *)(sb + ws.ICNT);
+    S.icls = (int32_t *)(sb + ws.ICLS);
+    return S;
+  };
+  auto gcn_args = [&](int64_t c, const Slot &S) {
+    const int64_t c0 = c * chunk, n = n_pairs - c0 < chunk ? n_pairs - c0 : chunk;
+    GcnArgs g = G;
+    g.pairs = pairs + 2 * c0;
+    g.inst = S.INST;
+    g.isorted = units ? S.isort : nullptr;
+    g.icls = units ? S.icls : nullptr;
+    g.X = S.X;
+    g.GX = S.GX;
+    g.n_pairs = n;
+    g.pair_offset = pair_offset + c0;
+    return g;
+  };
+  // chunk c's extents, unit order and forward instance kernel (stream st)
+  auto front = [&](int64_t c) -> int {
+    const Slot S = slot(c);
+    const int64_t c0 = c * chunk, n = n_pairs - c0 < chunk ? n_pairs - c0 : chunk;
     const int64_t nblk = (n + TB - 1) / TB;
-    const int32_t *pc = pairs + 2 * c0;
-    hipLaunchKernelGGL(web_ext_kernel, dim3((unsigned)nblk), dim3(TB), 0, st, pc, n,
-                       store->node_off, store->row_ptr, full, D, EXT, EXT16, EXT128, INST);
-    G.pairs = pc;
-    G.inst = INST;
-    G.isorted = nullptr;
-    G.icls = nullptr;
+    hipLaunchKernelGGL(web_ext_kernel, dim3((unsigned)nblk), dim3(TB), 0, st, pairs + 2 * c0, n,
+                       store->node_off, store->row_ptr, full, D, S.EXT, S.EXT16, S.EXT128, S.INST);
     if (units) {   // instance units: small instances share a workgroup (web_gcn_kernel)
       const int n16 = (store->n_max + 15) & ~15;
       const int cap4 = (n16 / 4) & ~15, cap2 = (n16 / 2) & ~15;
       const int nbu = (int)((2 * n + kUnitChunk - 1) / kUnitChunk);
-      int32_t *isort = (int32_t *)(base + ws.ISORT), *icnt = (int32_t *)(base + ws.ICNT);
-      int32_t *icls = (int32_t *)(base + ws.ICLS);
-      hipLaunchKernelGGL(web_icls_count, dim3(nbu), dim3(256), 0, st, INST, 2 * n, cap4, cap2,
-                         nbu, icnt);
-      hipLaunchKernelGGL(web_icls_scan, dim3(1), dim3(64), 0, st, icnt, nbu, 2 * n, icls);
-      hipLaunchKernelGGL(web_icls_scatter, dim3(nbu), dim3(256), 0, st, INST, 2 * n, cap4, cap2,
-                         nbu, (const int32_t *)icnt, isort);
-      G.isorted = isort;
-      G.icls = icls;
+      hipLaunchKernelGGL(web_icls_count, dim3(nbu), dim3(256), 0, st, S.INST, 2 * n, cap4, cap2,
+                         nbu, S.icnt);
+      hipLaunchKernelGGL(web_icls_scan, dim3(1), dim3(64), 0, st, S.icnt, nbu, 2 * n, S.icls);
+      hipLaunchKernelGGL(web_icls_scatter, dim3(nbu), dim3(256), 0, st, S.INST, 2 * n, cap4, cap2,
+                         nbu, (const int32_t *)S.icnt, S.isort);
     }
-    G.n_pairs = n;
-    G.pair_offset = pair_offset + c0;
-    if ((rc = gcn_launch(false, W, G, 2 * n, st)) != SG_OK) return rc;
+    return gcn_launch(false, W, gcn_args(c, S), 2 * n, st);
+  };
+  // chunk c's NTN GEMMs and head (stream gs)
+  auto middle = [&](int64_t c) {
+    const Slot S = slot(c);
+    const int64_t c0 = c * chunk, n = n_pairs - c0 < chunk ? n_pairs - c0 : chunk;
+    const int64_t nblk = (n + TB - 1) / TB;
+    float *X = S.X, *GX = S.GX, *T = S.T, *GM = S.GM;
     if (SG_WEB_T_BF3)
       hipLaunchKernelGGL(web_t_kernel_b3<true>, dim3((unsigned)nblk, Dp / TB, K), dim3(256), 0,
-                         st, X + ws.Cp * Dp, Wg, EXT128, n, Dp, K, T, X);
+                         gs, X + ws.Cp * Dp, Wg, S.EXT128, n, Dp, K, T, X);
     else
-      hipLaunchKernelGGL(web_t_kernel, dim3((unsigned)nblk, Dp / TB, K), dim3(256), 0, st,
-                         X + ws.Cp * Dp, Wg, EXT128, n, Dp, K, T);
-    H.n = n;
-    H.labels = labels ? labels + c0 : nullptr;
-    H.s_out = s_out ? s_out + c0 : nullptr;
+      hipLaunchKernelGGL(web_t_kernel, dim3((unsigned)nblk, Dp / TB, K), dim3(256), 0, gs,
+                         X + ws.Cp * Dp, Wg, S.EXT128, n, Dp, K, T);
+    HeadArgs h = H;
+    h.X = X; h.T = T; h.ext = S.EXT; h.ext128 = S.EXT128; h.GX = GX; h.GM = GM;
+    h.n = n;
+    h.labels = labels ? labels + c0 : nullptr;
+    h.s_out = s_out ? s_out + c0 : nullptr;
     const int hb = (int)((n + 3) / 4 < ws.head_blocks ? (n + 3) / 4 : ws.head_blocks);
     if (bwd) {
       if (SG_WEB_T_BF3) {
-        hipLaunchKernelGGL((web_head_kernel<true, true>), dim3(hb), dim3(256), head_lds, st, H);
-        hipLaunchKernelGGL(web_gx1_kernel_b3, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, st,
-                           X + ws.Cp * Dp, GM, Wg, EXT128, n, Dp, K, GX);
-        hipLaunchKernelGGL(web_gx2_kernel_b3, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, st, X,
-                           GM, Wh, EXT128, n, Dp, K, GX + ws.Cp * Dp);
-      } else {
-        hipLaunchKernelGGL((web_head_kernel<true, false>), dim3(hb), dim3(256), head_lds, st, H);
-        hipLaunchKernelGGL(web_gx2_kernel, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, st, X, GM,
-                           Wh, EXT128, n, Dp, K, GX + ws.Cp * Dp);
-      }
-      if (SG_WEB_T_BF3) {   // gV rides along
+        hipLaunchKernelGGL((web_head_kernel<true, true>), dim3(hb), dim3(256), head_lds, gs, h);
+        hipLaunchKernelGGL(web_gx1_kernel_b3, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, gs,
+                           X + ws.Cp * Dp, GM, Wg, S.EXT128, n, Dp, K, GX);
+        hipLaunchKernelGGL(web_gx2_kernel_b3, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, gs, X,
+                           GM, Wh, S.EXT128, n, Dp, K, GX + ws.Cp * Dp);
+        // gV rides along
         hipLaunchKernelGGL(web_wgrad_kernel_b3, dim3((Dp / TB) * (Dp / TB), K, WSPLIT), dim3(256),
-                           0, st, X, X + ws.Cp * Dp, GM, EXT16, n, Dp, K, GWS, GVS);
+                           0, gs, X, X + ws.Cp * Dp, GM, S.EXT16, n, Dp, K, GWS, GVS);
       } else {
+        hipLaunchKernelGGL((web_head_kernel<true, false>), dim3(hb), dim3(256), head_lds, gs, h);
+        hipLaunchKernelGGL(web_gx2_kernel, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, gs, X, GM,
+                           Wh, S.EXT128, n, Dp, K, GX + ws.Cp * Dp);
         hipLaunchKernelGGL(web_wgrad_kernel, dim3((Dp / TB) * (Dp / TB), K, WSPLIT), dim3(256), 0,
-                           st, X, X + ws.Cp * Dp, GM, EXT16, n, Dp, K, GWS);
-        hipLaunchKernelGGL(web_gv_kernel, dim3(2 * Dp / 64, WSPLIT), dim3(256), 0, st, X, GM, n,
+                           gs, X, X + ws.Cp * Dp, GM, S.EXT16, n, Dp, K, GWS);
+        hipLaunchKernelGGL(web_gv_kernel, dim3(2 * Dp / 64, WSPLIT), dim3(256), 0, gs, X, GM, n,
                            ws.Cp, Dp, K, GVS);
       }
-      if ((rc = gcn_launch(true, W, G, 2 * n, st)) != SG_OK) return rc;
     } else {
       if (SG_WEB_T_BF3)
-        hipLaunchKernelGGL((web_head_kernel<false, true>), dim3(hb), dim3(256), head_lds, st, H);
+        hipLaunchKernelGGL((web_head_kernel<false, true>), dim3(hb), dim3(256), head_lds, gs, h);
       else
-        hipLaunchKernelGGL((web_head_kernel<false, false>), dim3(hb), dim3(256), head_lds, st, H);
+        hipLaunchKernelGGL((web_head_kernel<false, false>), dim3(hb), dim3(256), head_lds, gs, h);
     }
+  };
+  // chunk c's backward instance kernel (stream st)
+  auto back = [&](int64_t c) -> int {
+    const Slot S = slot(c);
+    const int64_t n = n_pairs - c * chunk < chunk ? n_pairs - c * chunk : chunk;
+    return gcn_launch(true, W, gcn_args(c, S), 2 * n, st);
+  };
+  // enqueue order: front(c) after middle(c - 2) (slot reuse) | back(c - 1) after
+  // middle(c - 1) | middle(c) after front(c)
+  for (int64_t c = 0; c < nch; ++c) {
+    if (pipe && c >= 2 && hipStreamWaitEvent(st, evG[c & 1], 0) != hipSuccess) return SG_ERR_HIP;
+    if ((rc = front(c)) != SG_OK) return rc;
+    if (pipe && hipEventRecord(evF, st) != hipSuccess) return SG_ERR_HIP;
+    if (pipe && c > 0 && bwd) {
+      if (hipStreamWaitEvent(st, evG[(c - 1) & 1], 0) != hipSuccess) return SG_ERR_HIP;
+      if ((rc = back(c - 1)) != SG_OK) return rc;
+    }
+    if (pipe && hipStreamWaitEvent(gs, evF, 0) != hipSuccess) return SG_ERR_HIP;
+    middle(c);
+    if (pipe && hipEventRecord(evG[c & 1], gs) != hipSuccess) return SG_ERR_HIP;
+    if (!pipe && bwd && (rc = back(c)) != SG_OK) return rc;
+  }
+  if (pipe) {   // join: st waits for the last chunk's GEMMs (gs runs them in order)
+    if (hipStreamWaitEvent(st, evG[(nch - 1) & 1], 0) != hipSuccess) return SG_ERR_HIP;
+    if (bwd && (rc = back(nch - 1)) != SG_OK) return rc;
   }
   if (!bwd) return web_status();
 

@@ -123,6 +123,25 @@ def test_web_chunks_shards_determinism(gpu):
     assert abs(l0 + float(model.loss_buf[0].item()) - l_full) <= 1e-5 * max(1.0, abs(l_full))
 
 
+def test_web_pipeline_is_bitwise_the_serial_sequence(gpu, monkeypatch):
+    """The two-stream chunk pipeline (forward instance kernel of chunk c + 1 beside the
+    NTN GEMMs of chunk c, two workspace slots) gives the bits of the one-stream sequence:
+    scores, gradient and loss, forward and fwd_bwd, over several chunks."""
+    import torch
+    prob = small_problem(n_graphs=24, n_pairs=700, seed=13, n_lo=20, n_hi=128, n_max=128,
+                         p_extra=0.05)
+    model, chunked = prob.make_gpu_web_model(device=gpu, chunk=97)
+    out = {}
+    for mode in ('1', '0'):
+        monkeypatch.setenv('SG_WEB_PIPE', mode)
+        s = model.pred_sim_without_act(chunked, seed=9).clone()
+        model.fwd_bwd(chunked, seed=9)
+        torch.cuda.synchronize()
+        out[mode] = (s, model.grad.clone(), model.loss_buf.clone())
+    for a, b in zip(out['1'], out['0']):
+        assert torch.equal(a, b)
+
+
 def test_web_empty_batch(gpu):
     prob = _problem('d64')
     model, batch = prob.make_gpu_web_model(device=gpu)
