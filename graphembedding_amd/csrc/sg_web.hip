@@ -50,6 +50,12 @@ constexpr int KMS = TB + 4;         // KM LDS tile row stride
 constexpr int HSLAB = 1 + 2 * WKP;  // head slab row: loss | gU[16] | gb[16]
 constexpr int WSPLIT = 8;           // split-K over pairs of the weight-gradient GEMMs
 constexpr int kUnitChunk = 4096;    // instances per block of the size-class sort (web_icls_*)
+// XCD partitions of the instance units: instances of graph g go to partition g % kXcdParts,
+// and unit slot u runs on the workgroups with blockIdx.x = u (mod kXcdParts), which the
+// dispatcher deals to one XCD (observed placement; speed only, never correctness): each
+// XCD then gathers the CSR rows of an eighth of the graphs, which fit its 4 MiB L2
+constexpr int kXcdParts = 8;
+constexpr int kIKeys = 3 * kXcdParts;   // sort keys: size class x partition
 
 struct WebPlan {
   int d_in, D, Dp, K;
@@ -166,8 +172,8 @@ WebWs web_ws(const WebPlan &W, int64_t chunk) {
   w.EXT128 = take(2 * (w.Cp / TB));
   w.INST = take(8 * w.Cp);          // int4 per instance
   w.ISORT = take(2 * w.Cp);         // instances sorted by size class
-  w.ICNT = take(3 * ((2 * w.Cp + kUnitChunk - 1) / kUnitChunk));
-  w.ICLS = take(4);
+  w.ICNT = take(kIKeys * ((2 * w.Cp + kUnitChunk - 1) / kUnitChunk));
+  w.ICLS = take(kIKeys + 8);
   w.SLOT = o;
   o += w.SLOT;                      // slot 1
   w.Wg = take(K * Dp * Dp);
@@ -227,36 +233,44 @@ __global__ void __launch_bounds__(TB) web_ext_kernel(const int32_t *__restrict__
 }
 
 // ---------------------------------------------------------------------------
-// Instance size classes for the instance kernels' units (GcnArgs::isorted): a stable
-// counting sort of the chunk's instances by class (0: N <= cap4, 1: N <= cap2, 2: the
-// rest; cap4 / cap2 = a quarter / half of the instance region).  Blocks own contiguous
-// runs of kUnitChunk instances; counts are key-major so one exclusive scan gives every
-// (class, run) its base; the scatter ranks by ballot: deterministic.
+// Instance units for the instance kernels (GcnArgs::isorted): a stable counting sort of
+// the chunk's instances by key = size class (0: N <= cap4, 1: N <= cap2, 2: the rest;
+// cap4 / cap2 = a quarter / half of the instance region) x XCD partition (graph % np,
+// np = kXcdParts, or 1 with SG_WEB_XCD=0).  Blocks own contiguous runs of kUnitChunk
+// instances; counts are key-major so one exclusive scan gives every (key, run) its base;
+// the scatter ranks by ballot: deterministic.  Instance q is side q & 1 of pair q >> 1,
+// whose graph is pairs[q].
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int web_icls(const int4 *inst, int64_t q, int cap4, int cap2) {
+__device__ __forceinline__ int web_ikey(const int4 *inst, const int32_t *pairs, int64_t q,
+                                        int cap4, int cap2, int np) {
   const int N = inst[q].y;
-  return N <= cap4 ? 0 : (N <= cap2 ? 1 : 2);
+  const int c = N <= cap4 ? 0 : (N <= cap2 ? 1 : 2);
+  return c * kXcdParts + (np > 1 ? (int)((uint32_t)pairs[q] % (uint32_t)np) : 0);
 }
 
-__global__ void __launch_bounds__(256) web_icls_count(const int4 *__restrict__ inst, int64_t n,
-                                                      int cap4, int cap2, int nb,
+__global__ void __launch_bounds__(256) web_icls_count(const int4 *__restrict__ inst,
+                                                      const int32_t *__restrict__ pairs, int64_t n,
+                                                      int cap4, int cap2, int np, int nb,
                                                       int32_t *__restrict__ cnt) {
-  __shared__ int h[3];
-  if (threadIdx.x < 3) h[threadIdx.x] = 0;
+  __shared__ int h[kIKeys];
+  if (threadIdx.x < kIKeys) h[threadIdx.x] = 0;
   __syncthreads();
   const int64_t b0 = (int64_t)blockIdx.x * kUnitChunk;
   for (int i = threadIdx.x; i < kUnitChunk && b0 + i < n; i += blockDim.x)
-    atomicAdd(&h[web_icls(inst, b0 + i, cap4, cap2)], 1);
+    atomicAdd(&h[web_ikey(inst, pairs, b0 + i, cap4, cap2, np)], 1);
   __syncthreads();
-  if (threadIdx.x < 3) cnt[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
+  if (threadIdx.x < kIKeys) cnt[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
 }
 
-// exclusive scan of the 3 nb counts (small: one thread), and the class starts
-__global__ void web_icls_scan(int32_t *__restrict__ cnt, int nb, int64_t n,
+// exclusive scan of the kIKeys x nb counts (small: one thread), the key starts
+// icls[0..kIKeys], and the unit-slot layout: class c holds np x R_c unit slots from
+// icls[kIKeys + 1 + c] (R_c = the most units of any of its partitions; units of 4, 2 and
+// 1 instances for classes 0, 1, 2), icls[kIKeys + 4] = all slots, icls[kIKeys + 5] = np
+__global__ void web_icls_scan(int32_t *__restrict__ cnt, int nb, int64_t n, int np,
                               int32_t *__restrict__ icls) {
   if (threadIdx.x != 0) return;
   int run = 0;
-  for (int k = 0; k < 3; ++k) {
+  for (int k = 0; k < kIKeys; ++k) {
     icls[k] = run;
     for (int b = 0; b < nb; ++b) {
       const int v = cnt[(size_t)k * nb + b];
@@ -264,29 +278,44 @@ __global__ void web_icls_scan(int32_t *__restrict__ cnt, int nb, int64_t n,
       run += v;
     }
   }
-  icls[3] = (int32_t)n;
+  icls[kIKeys] = (int32_t)n;
+  int ub = 0;
+  for (int c = 0; c < 3; ++c) {
+    const int gsz = c == 0 ? 4 : (c == 1 ? 2 : 1);
+    int R = 0;
+    for (int p = 0; p < np; ++p) {
+      const int k = c * kXcdParts + p;
+      const int nu = (icls[k + 1] - icls[k] + gsz - 1) / gsz;
+      R = nu > R ? nu : R;
+    }
+    icls[kIKeys + 1 + c] = ub;
+    ub += np * R;
+  }
+  icls[kIKeys + 4] = ub;
+  icls[kIKeys + 5] = np;
 }
 
-__global__ void __launch_bounds__(256) web_icls_scatter(const int4 *__restrict__ inst, int64_t n,
-                                                        int cap4, int cap2, int nb,
+__global__ void __launch_bounds__(256) web_icls_scatter(const int4 *__restrict__ inst,
+                                                        const int32_t *__restrict__ pairs, int64_t n,
+                                                        int cap4, int cap2, int np, int nb,
                                                         const int32_t *__restrict__ base,
                                                         int32_t *__restrict__ sorted) {
-  __shared__ int run[3];
-  __shared__ int wc[4][3];
+  __shared__ int run[kIKeys];
+  __shared__ int wc[4][kIKeys];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  if (t < 3) run[t] = base[(size_t)t * nb + blockIdx.x];
+  if (t < kIKeys) run[t] = base[(size_t)t * nb + blockIdx.x];
   const int64_t b0 = (int64_t)blockIdx.x * kUnitChunk;
   const int64_t b1 = b0 + kUnitChunk < n ? b0 + kUnitChunk : n;
   for (int64_t t0 = b0; t0 < b1; t0 += 256) {
-    if (t < 12) (&wc[0][0])[t] = 0;
+    if (t < 4 * kIKeys) (&wc[0][0])[t] = 0;
     __syncthreads();
     const int64_t q = t0 + t;
     const bool valid = q < b1;
-    const int key = valid ? web_icls(inst, q, cap4, cap2) : -1;
+    const int key = valid ? web_ikey(inst, pairs, q, cap4, cap2, np) : -1;
     int rank = 0;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < kIKeys; ++k) {
       const uint64_t m = __ballot(valid && key == k);
+      if (m == 0ull) continue;   // wave-uniform
       if (key == k) rank = __popcll(m & ((1ull << lane) - 1ull));
       if (lane == 0) wc[w][k] = __popcll(m);
     }
@@ -297,7 +326,7 @@ __global__ void __launch_bounds__(256) web_icls_scatter(const int4 *__restrict__
       sorted[off] = (int32_t)q;
     }
     __syncthreads();
-    if (t < 3) run[t] += wc[0][t] + wc[1][t] + wc[2][t] + wc[3][t];
+    if (t < kIKeys) run[t] += wc[0][t] + wc[1][t] + wc[2][t] + wc[3][t];
     __syncthreads();
   }
 }
@@ -361,11 +390,12 @@ struct GcnArgs {
   const float *val;
   const int32_t *pairs;
   const int4 *inst;  // [2 n_pairs] (first node, nodes, first Â entry, Â entries) per instance
-  // Units (web_units): the chunk's instances stable-sorted by size class (isorted) with
-  // the class starts icls[0..3] (class 0: N <= cap/4, 1: N <= cap/2, 2: larger; cap =
-  // the instance region of n_max nodes).  A workgroup takes a unit of 4, 2 or 1
-  // instances of one class and gives each a quarter / half / all of its waves and of
-  // its instance region: the latency-bound phases of small instances overlap.
+  // Units (web_units): the chunk's instances stable-sorted by size class x XCD partition
+  // (isorted) with the key starts and unit-slot layout in icls (web_icls_scan; class 0:
+  // N <= cap/4, 1: N <= cap/2, 2: larger; cap = the instance region of n_max nodes).  A
+  // workgroup takes a unit of 4, 2 or 1 instances of one class and partition and gives
+  // each a quarter / half / all of its waves and of its instance region: the
+  // latency-bound phases of small instances overlap.
   // isorted == null: units of one instance in list order.
   const int32_t *isorted;
   const int32_t *icls;
@@ -391,6 +421,15 @@ struct GcnArgs {
 // LDS row strides (words): not multiples of 16, so the random-row b128 gathers of
 // the sparse products spread over the banks (stride 16 puts every row on 4 bank groups)
 constexpr int W0S = 36, ZS = 20, DS = 36;
+// a wave's scratch tile (backward): 16 rows at stride SCS (≡ 20 mod 64 words: the column
+// reads (4g + s)·SCS + i of lanes (i, g) hit distinct banks; stride 16 put 4 rows g on one)
+constexpr int SCS = 20, SCR = 16 * SCS;
+// gS0 = Â·gP0 with one CSR row per lane (node 16t + i, features 16c + 4g + s) and the tile
+// transposed through the wave's scratch for the one-hot gW0 MFMA; 0: four rows per lane
+// (nodes 16t + 4g + s, features i, 16 + i), the MFMA layout directly
+#ifndef SG_WEB_GS0_ROW
+#define SG_WEB_GS0_ROW 1
+#endif
 
 struct GcnLds {
   int w0, b0, w1, w1t, b1, wd, tables, et, gx, z1, d1, scr, rp, col, val, total;
@@ -411,7 +450,7 @@ __host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, int max_nnz, bool b
   L.gx = o; if (bwd) o += n16;
   L.z1 = o; o += n16 * ZS;
   L.d1 = o; if (bwd) o += n16 * DS;
-  L.scr = o; if (bwd) o += gcn_gw(true) * 256;
+  L.scr = o; if (bwd) o += gcn_gw(true) * SCR;
   L.rp = o; if (lcsr) o += (n16 + 4) & ~3;
   L.col = o; if (lcsr) o += ((max_nnz + 1) / 2 + 3) & ~3;   // u16 columns
   L.val = o; if (lcsr) o += (max_nnz + 3) & ~3;
@@ -420,6 +459,8 @@ __host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, int max_nnz, bool b
 }
 
 // Σ_e val[e] · f(col[e]) over one CSR row, four neighbours' loads in flight at a time
+// (eight per step with a clamped, masked last step measured 3.20 vs 3.89 M pairs/s on C5,
+// profiles/r03_c5ab/)
 template <typename CT, typename F>
 __device__ __forceinline__ void csr_row(const CT *__restrict__ col, const float *__restrict__ val,
                                         int e0, int e1, F f) {
@@ -435,17 +476,21 @@ __device__ __forceinline__ void csr_row(const CT *__restrict__ col, const float 
   for (; e < e1; ++e) f(col[e], val[e]);
 }
 
-// instance (.x, -1: none) of wave w in unit u of the size-class-sorted list, and the
-// unit size (.y): units of 4 class-0 instances, then of 2 class-1, then single ones
-__device__ __forceinline__ int2 web_unit_q(int u, const int32_t *isorted, int ni, int c1, int c2,
-                                           int U0, int U1, int n_units, int w, int gw) {
+// instance (.x, -1: none) of wave w in unit slot u of the partitioned size-class order
+// (web_icls_scan), and the unit size (.y): class c's slots start at ub_c; slot ub_c +
+// np r + p is unit r of key (c, p), i.e. instances icls[k] + gsz r .. of the sorted list,
+// or empty when partition p has fewer units.  With np = kXcdParts and gridDim.x a multiple
+// of it, every unit of partition p runs on the XCD of blocks b = p (mod np).
+__device__ __forceinline__ int2 web_unit_q(int u, const int32_t *isorted, const int32_t *icls, int ni,
+                                           int ub1, int ub2, int np, int n_units, int w, int gw) {
   if (!isorted) return make_int2(u < ni ? u : -1, 1);
-  const bool a0 = u < U0, a1 = !a0 && u < U0 + U1;
+  const bool a0 = u < ub1, a1 = !a0 && u < ub2;
   const int gsz = a0 ? 4 : (a1 ? 2 : 1);
-  const int s0 = a0 ? 4 * u : (a1 ? c1 + 2 * (u - U0) : c2 + (u - U0 - U1));
-  const int end = a0 ? c1 : (a1 ? c2 : ni);
-  const int k = w / (gw / gsz);
-  return make_int2((u < n_units && s0 + k < end) ? isorted[s0 + k] : -1, gsz);
+  const int rel = u - (a0 ? 0 : (a1 ? ub1 : ub2));
+  const int r = rel / np, k = (a0 ? 0 : (a1 ? 1 : 2)) * kXcdParts + (rel - r * np);
+  const int s0 = icls[k] + r * gsz, end = icls[k + 1];
+  const int kk = w / (gw / gsz);
+  return make_int2((u < n_units && s0 + kk < end) ? isorted[s0 + kk] : -1, gsz);
 }
 
 template <bool BWD, int NTB, bool LCSR>
@@ -461,7 +506,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
   float *sW0 = sm + L.w0, *sb0 = sm + L.b0, *sW1 = sm + L.w1, *sW1T = sm + L.w1t;
   float *sb1 = sm + L.b1, *sWd = sm + L.wd;
   int *sEt = (int *)(sm + L.et);
-  float *sZ1 = sm + L.z1, *sD1 = sm + L.d1, *scr = sm + L.scr + w * 256;
+  float *sZ1 = sm + L.z1, *sD1 = sm + L.d1, *scr = sm + L.scr + w * SCR;
   int *sRp = (int *)(sm + L.rp);
   uint16_t *sCol = (uint16_t *)(sm + L.col);
   float *sVal = sm + L.val;
@@ -502,18 +547,18 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
   const float *const gval = A.val, *const gGX = A.GX;
   const int64_t gCp = A.Cp;
   const int gDp = A.Dp;
-  int c1 = ni, c2 = ni, U0 = 0, U1 = 0, n_units = ni;
+  const int32_t *const icls = A.icls;
+  int ub1 = ni, ub2 = ni, np = 1, n_units = ni;
   if (isorted) {
-    c1 = __builtin_amdgcn_readfirstlane(A.icls[1]);
-    c2 = __builtin_amdgcn_readfirstlane(A.icls[2]);
-    U0 = (c1 + 3) >> 2;
-    U1 = (c2 - c1 + 1) >> 1;
-    n_units = U0 + U1 + (ni - c2);
+    ub1 = __builtin_amdgcn_readfirstlane(icls[kIKeys + 2]);
+    ub2 = __builtin_amdgcn_readfirstlane(icls[kIKeys + 3]);
+    n_units = __builtin_amdgcn_readfirstlane(icls[kIKeys + 4]);
+    np = __builtin_amdgcn_readfirstlane(icls[kIKeys + 5]);
   }
   // this thread's instance of unit u (.x, -1: none) and the unit size (.y): a plain
   // function of values (a lambda's closure got its selects turned into loads from scratch)
   auto unit_q = [&](int u) __attribute__((always_inline)) -> int2 {
-    return web_unit_q(u, isorted, ni, c1, c2, U0, U1, n_units, w, GW_);
+    return web_unit_q(u, isorted, icls, ni, ub1, ub2, np, n_units, w, GW_);
   };
 
   // The next unit's inputs are prefetched into registers while this one computes:
@@ -731,12 +776,12 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) gd[cb] = mfma4(q4[s], sW1T[(4 * g + s) * WH1 + 16 * cb + i], gd[cb]);
       // the tile's gS1 through the wave's scratch, read back as the B operand of gW1
-      *(float4 *)(scr + i * WH2 + 4 * g) = make_float4(q4[0], q4[1], q4[2], q4[3]);
+      *(float4 *)(scr + i * SCS + 4 * g) = make_float4(q4[0], q4[1], q4[2], q4[3]);
       sg_wsync();
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int nn = 16 * t + 4 * g + s;
-        const float b = scr[(4 * g + s) * WH2 + i];
+        const float b = scr[(4 * g + s) * SCS + i];
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) aW1[cb] = mfma4(sD1k[nn * DS + 16 * cb + i], b, aW1[cb]);
       }
@@ -754,11 +799,51 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
     }
     __syncthreads();
 
-    // ---- gS0 = Â·gP0 (rows n = 16t + 4g + s, features i, 16 + i); gW0 += Xᵀ·(scale0·gS0) ----
+    // ---- gS0 = Â·gP0; gW0 += Xᵀ·(scale0·gS0) ----
 #pragma unroll
     for (int u = 0; u < GCN_TPW; ++u) {
       const int t = lw + u * WPI;
       if (t >= ntile) break;
+#if SG_WEB_GS0_ROW
+      // one CSR row per lane: node n = 16t + i, features 16c + 4g + s (two b128 reads of
+      // the gP0 row per entry); dropped and absent nodes (et = d_in) contribute zero
+      float hq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      {
+        const int n = 16 * t + i;
+        if (n < N && sEtk[n] < d_in)
+          csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
+            const float *dr = sD1k + mm * DS + 4 * g;
+            const float4 da = *(const float4 *)dr, db = *(const float4 *)(dr + 16);
+            hq[0] = fmaf(v, da.x, hq[0]); hq[1] = fmaf(v, da.y, hq[1]);
+            hq[2] = fmaf(v, da.z, hq[2]); hq[3] = fmaf(v, da.w, hq[3]);
+            hq[4] = fmaf(v, db.x, hq[4]); hq[5] = fmaf(v, db.y, hq[5]);
+            hq[6] = fmaf(v, db.z, hq[6]); hq[7] = fmaf(v, db.w, hq[7]);
+          });
+      }
+      int et[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) et[s] = sEtk[16 * t + 4 * g + s];
+      // per feature half c: the tile through the scratch, read back as the B operand
+      // (k-slot g ↔ node 16t + 4g + s, column i ↔ feature 16c + i)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        *(float4 *)(scr + i * SCS + 4 * g) =
+            make_float4(hq[4 * c] * A.ik0, hq[4 * c + 1] * A.ik0, hq[4 * c + 2] * A.ik0,
+                        hq[4 * c + 3] * A.ik0);
+        sg_wsync();
+        float bq[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) bq[s] = scr[(4 * g + s) * SCS + i];
+        sg_wsync();
+#pragma unroll
+        for (int tb = 0; tb < NTB; ++tb)
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const float a = et[s] == 16 * tb + i ? 1.f : 0.f;
+            aW0[tb][c] = mfma4(a, bq[s], aW0[tb][c]);
+          }
+      }
+#else
       float bq[4][2];
       int et[4];
 #pragma unroll
@@ -782,6 +867,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
           aW0[tb][0] = mfma4(a, bq[s][0], aW0[tb][0]);
           aW0[tb][1] = mfma4(a, bq[s][1], aW0[tb][1]);
         }
+#endif
     }
     in = inn;
     q = qn;
@@ -1925,6 +2011,11 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     const char *e = getenv("SG_WEB_UNITS");
     return !(e && e[0] == '0');
   }();
+  // XCD partitions of the units, opt-in (SG_WEB_XCD=1; read per call: a test compares the
+  // two).  Measured 2% slower on C5 than the plain size-class order (3.81-3.83 vs 3.88 M
+  // pairs/s, profiles/r03_c5v1): the partitions' work differs by XCD
+  const char *xcd_e = getenv("SG_WEB_XCD");
+  const int xparts = (xcd_e && xcd_e[0] == '1') ? kXcdParts : 1;
 
   // Two-stream pipeline over the chunks.  The instance kernels are latency-bound (most
   // wave cycles wait on the CSR gathers) and the NTN GEMMs are MFMA work, so the forward
@@ -1982,11 +2073,13 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
       const int n16 = (store->n_max + 15) & ~15;
       const int cap4 = (n16 / 4) & ~15, cap2 = (n16 / 2) & ~15;
       const int nbu = (int)((2 * n + kUnitChunk - 1) / kUnitChunk);
-      hipLaunchKernelGGL(web_icls_count, dim3(nbu), dim3(256), 0, st, S.INST, 2 * n, cap4, cap2,
-                         nbu, S.icnt);
-      hipLaunchKernelGGL(web_icls_scan, dim3(1), dim3(64), 0, st, S.icnt, nbu, 2 * n, S.icls);
-      hipLaunchKernelGGL(web_icls_scatter, dim3(nbu), dim3(256), 0, st, S.INST, 2 * n, cap4, cap2,
-                         nbu, (const int32_t *)S.icnt, S.isort);
+      const int32_t *cp = pairs + 2 * c0;
+      hipLaunchKernelGGL(web_icls_count, dim3(nbu), dim3(256), 0, st, S.INST, cp, 2 * n, cap4,
+                         cap2, xparts, nbu, S.icnt);
+      hipLaunchKernelGGL(web_icls_scan, dim3(1), dim3(64), 0, st, S.icnt, nbu, 2 * n, xparts,
+                         S.icls);
+      hipLaunchKernelGGL(web_icls_scatter, dim3(nbu), dim3(256), 0, st, S.INST, cp, 2 * n, cap4,
+                         cap2, xparts, nbu, (const int32_t *)S.icnt, S.isort);
     }
     return gcn_launch(false, W, gcn_args(c, S), 2 * n, st);
   };

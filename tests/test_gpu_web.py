@@ -142,6 +142,31 @@ def test_web_pipeline_is_bitwise_the_serial_sequence(gpu, monkeypatch):
         assert torch.equal(a, b)
 
 
+def test_web_xcd_units_match_flat_units(gpu, monkeypatch):
+    """The XCD-partitioned unit order (instances of graph g on the blocks of partition
+    g % 8) changes only which workgroup runs an instance: scores and loss are bitwise
+    those of the plain size-class order, the gradient equal up to the order of the
+    per-block sums (and bitwise reproducible)."""
+    import torch
+    prob = small_problem(n_graphs=40, n_pairs=900, seed=21, n_lo=8, n_hi=128, n_max=128,
+                         p_extra=0.05)
+    model, chunked = prob.make_gpu_web_model(device=gpu, chunk=301)
+    out = {}
+    for mode in ('1', '0', '1'):
+        monkeypatch.setenv('SG_WEB_XCD', mode)
+        s = model.pred_sim_without_act(chunked, seed=5).clone()
+        model.fwd_bwd(chunked, seed=5)
+        torch.cuda.synchronize()
+        r = (s, model.grad.clone(), model.loss_buf.clone())
+        if mode in out:
+            assert all(torch.equal(a, b) for a, b in zip(out[mode], r))
+        out[mode] = r
+    (s1, g1, l1), (s0, g0, l0) = out['1'], out['0']
+    assert torch.equal(s1, s0)
+    assert torch.equal(l1, l0)
+    _check_grad(g1.cpu().numpy(), g0.cpu().numpy(), prob, tol=1e-5)
+
+
 def test_web_empty_batch(gpu):
     prob = _problem('d64')
     model, batch = prob.make_gpu_web_model(device=gpu)
