@@ -458,13 +458,37 @@ __host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, int max_nnz, bool b
   return L;
 }
 
-// Σ_e val[e] · f(col[e]) over one CSR row, four neighbours' loads in flight at a time
-// (eight per step with a clamped, masked last step measured 3.20 vs 3.89 M pairs/s on C5,
-// profiles/r03_c5ab/)
+// Σ_e val[e] · f(col[e]) over one CSR row.  SG_WEB_ROWP = 0 (default): four neighbours'
+// loads in flight at a time, then the tail one entry at a time; SG_WEB_ROWP = w > 0: w
+// entries per step with no branch inside the step (indices past the row clamped to its last
+// entry, their value read as 0: fmaf(0, x, acc) = acc), so a row of up to w entries is one
+// global round trip.  Measured on C5 (profiles/r03_c5ab/): w = 4 2.97, w = 8 2.65 against
+// 3.88 M pairs/s, and eight entries with a branch around each call 3.20: the padded entries'
+// LDS gathers cost more than the round trips they save.
+#ifndef SG_WEB_ROWP
+#define SG_WEB_ROWP 0
+#endif
 template <typename CT, typename F>
 __device__ __forceinline__ void csr_row(const CT *__restrict__ col, const float *__restrict__ val,
                                         int e0, int e1, F f) {
   int e = e0;
+#if SG_WEB_ROWP > 0
+  constexpr int RW = SG_WEB_ROWP;
+  for (; e < e1; e += RW) {
+    int c[RW];
+    float v[RW];
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+      const bool in = e + k < e1;
+      const int ek = in ? e + k : e1 - 1;
+      c[k] = col[ek];
+      const float x = val[ek];
+      v[k] = in ? x : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < RW; ++k) f(c[k], v[k]);
+  }
+#else
   for (; e + 4 <= e1; e += 4) {
     const int c0 = col[e], c1 = col[e + 1], c2 = col[e + 2], c3 = col[e + 3];
     const float v0 = val[e], v1 = val[e + 1], v2 = val[e + 2], v3 = val[e + 3];
@@ -474,6 +498,7 @@ __device__ __forceinline__ void csr_row(const CT *__restrict__ col, const float 
     f(c3, v3);
   }
   for (; e < e1; ++e) f(col[e], val[e]);
+#endif
 }
 
 // instance (.x, -1: none) of wave w in unit slot u of the partitioned size-class order
