@@ -143,6 +143,7 @@ struct WebWs {
   // instance kernels of chunk c + 1 overlap the NTN GEMMs of chunk c (sg_web_run)
   int64_t X, GX, T, GM, EXT, EXT16, EXT128, INST;
   int64_t ISORT, ICNT, ICLS;                         // instance units (web_icls_*)
+  int64_t MASK;   // uint16 [2 Cp][Dp][4]: the forward's dropout keep bits per (instance, node, g)
   int64_t SLOT;                                      // floats per slot
   int64_t Wg, Wh, GWS, GVS, GSLAB, HSLABo, total;    // per-call buffers
   int gcn_blocks, head_blocks;
@@ -174,6 +175,7 @@ WebWs web_ws(const WebPlan &W, int64_t chunk) {
   w.ISORT = take(2 * w.Cp);         // instances sorted by size class
   w.ICNT = take(kIKeys * ((2 * w.Cp + kUnitChunk - 1) / kUnitChunk));
   w.ICLS = take(kIKeys + 8);
+  w.MASK = take(4 * w.Cp * Dp);     // 2 Cp x Dp x 4 uint16
   w.SLOT = o;
   o += w.SLOT;                      // slot 1
   w.Wg = take(K * Dp * Dp);
@@ -262,22 +264,42 @@ __global__ void __launch_bounds__(256) web_icls_count(const int4 *__restrict__ i
   if (threadIdx.x < kIKeys) cnt[(size_t)threadIdx.x * nb + blockIdx.x] = h[threadIdx.x];
 }
 
-// exclusive scan of the kIKeys x nb counts (small: one thread), the key starts
-// icls[0..kIKeys], and the unit-slot layout: class c holds np x R_c unit slots from
-// icls[kIKeys + 1 + c] (R_c = the most units of any of its partitions; units of 4, 2 and
-// 1 instances for classes 0, 1, 2), icls[kIKeys + 4] = all slots, icls[kIKeys + 5] = np
-__global__ void web_icls_scan(int32_t *__restrict__ cnt, int nb, int64_t n, int np,
-                              int32_t *__restrict__ icls) {
-  if (threadIdx.x != 0) return;
-  int run = 0;
-  for (int k = 0; k < kIKeys; ++k) {
-    icls[k] = run;
-    for (int b = 0; b < nb; ++b) {
-      const int v = cnt[(size_t)k * nb + b];
-      cnt[(size_t)k * nb + b] = run;
+// exclusive scan of the kIKeys x nb counts (one 1024-thread block: each thread sums a run of
+// consecutive counts, a block scan of the run sums, then each thread rewrites its run), the
+// key starts icls[0..kIKeys], and the unit-slot layout: class c holds np x R_c unit slots
+// from icls[kIKeys + 1 + c] (R_c = the most units of any of its partitions; units of 4, 2
+// and 1 instances for classes 0, 1, 2), icls[kIKeys + 4] = all slots, icls[kIKeys + 5] = np.
+// (A one-thread scan over the 24 x nb counts took 0.6 ms per 262,144-pair chunk.)
+constexpr int kScanT = 1024;
+__global__ void __launch_bounds__(kScanT) web_icls_scan(int32_t *__restrict__ cnt, int nb, int64_t n,
+                                                        int np, int32_t *__restrict__ icls) {
+  __shared__ int part[kScanT];
+  const int t = threadIdx.x;
+  const int tot = kIKeys * nb, per = (tot + kScanT - 1) / kScanT, b0 = t * per;
+  int sum = 0;
+  for (int k = 0; k < per; ++k)
+    if (b0 + k < tot) sum += cnt[b0 + k];
+  part[t] = sum;
+  __syncthreads();
+  for (int o = 1; o < kScanT; o <<= 1) {   // inclusive Hillis-Steele scan of the run sums
+    const int v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = t ? part[t - 1] : 0;
+  for (int k = 0; k < per; ++k) {
+    const int x = b0 + k;
+    if (x < tot) {
+      const int v = cnt[x];
+      cnt[x] = run;
+      if (x % nb == 0) icls[x / nb] = run;   // key x / nb starts here
       run += v;
     }
   }
+  if (tot == 0 && t < kIKeys) icls[t] = 0;
+  __syncthreads();   // the block's global writes of icls are visible to thread 0
+  if (t != 0) return;
   icls[kIKeys] = (int32_t)n;
   int ub = 0;
   for (int c = 0; c < 3; ++c) {
@@ -402,6 +424,10 @@ struct GcnArgs {
   int64_t n_pairs, pair_offset, Cp;
   const float *params;
   float *X;          // [2][Cp][Dp] NTN inputs (forward)
+  // [2 n_pairs][Dp][4] dropout keep bits of lane g of node n of instance q (or null): the
+  // forward writes them, the backward reads them instead of re-hashing.  Bits 4c + s: layer 1,
+  // feature 16c + 4g + s; 8 + s: layer 2, feature 4g + s; 12: layer 4 (the node's NTN input)
+  uint16_t *masks;
   const float *GX;   // [2][Cp][Dp] ∂L/∂x (backward)
   float *slab;       // [gridDim.x][n_gcn] (backward, accumulated)
   uint32_t key, thr0, thr1, thr2, thr4;
@@ -457,6 +483,12 @@ __host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, int max_nnz, bool b
   L.total = o;
   return L;
 }
+
+// The backward instance kernel reads the dropout keep bits the forward wrote (GcnArgs::masks)
+// instead of re-hashing 13 elements per lane and tile; 0: it re-hashes (A/B)
+#ifndef SG_WEB_MASKS
+#define SG_WEB_MASKS 1
+#endif
 
 // Σ_e val[e] · f(col[e]) over one CSR row.  SG_WEB_ROWP = 0 (default): four neighbours'
 // loads in flight at a time, then the tail one entry at a time; SG_WEB_ROWP = w > 0: w
@@ -636,6 +668,15 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
     const int n16 = (N + 15) & ~15;
     const int ntile = n16 >> 4;
     const uint32_t pk = sg_pair_key(A.key, (uint32_t)(A.pair_offset + p));
+    // dropout keep bits of this lane's tiles: the backward loads the forward's (their
+    // latency overlaps the staging below), the forward builds them
+    uint32_t mw[GCN_TPW];
+    constexpr bool use_mw = BWD && SG_WEB_MASKS;   // sg_web_run passes masks then
+#pragma unroll
+    for (int u = 0; u < GCN_TPW; ++u) {
+      const int n = 16 * (lw + u * WPI) + i;
+      mw[u] = (use_mw && n < N) ? (uint32_t)A.masks[((size_t)q * A.Dp + n) * 4 + g] : 0u;
+    }
     const int *rp;
     const ColT *cl;
     const float *vl;
@@ -692,7 +733,10 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
           for (int s = 0; s < 4; ++s) {
             const int f = 16 * c + 4 * g + s;
             const float hv = h[4 * c + s] > 0.f ? h[4 * c + s] : 0.f;
-            h[4 * c + s] = sg_keep(pk, 1, side, (uint32_t)(n * WH1 + f), A.thr1) ? hv : 0.f;
+            const bool k1 = use_mw ? ((mw[u] >> (4 * c + s)) & 1u) != 0u
+                                   : sg_keep(pk, 1, side, (uint32_t)(n * WH1 + f), A.thr1);
+            if (!BWD) mw[u] |= (k1 ? 1u : 0u) << (4 * c + s);
+            h[4 * c + s] = k1 ? hv : 0.f;
           }
       } else {
 #pragma unroll
@@ -737,15 +781,20 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
       float part = 0.f;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        k2[s] = sg_keep(pk, 2, side, (uint32_t)(n * WH2 + 4 * g + s), A.thr2);
+        k2[s] = use_mw ? ((mw[u] >> (8 + s)) & 1u) != 0u
+                       : sg_keep(pk, 2, side, (uint32_t)(n * WH2 + 4 * g + s), A.thr2);
+        if (!BWD) mw[u] |= (k2[s] ? 1u : 0u) << (8 + s);
         part = fmaf(k2[s] ? h2[s] : 0.f, sWd[4 * g + s], part);
       }
       const float pre = sgk::xsum32(sgk::xsum16(part)) + bd;
       const float z = pre > 0.f ? pre : 0.f;
-      const bool k4 = n < N && sg_keep(pk, 4, side, (uint32_t)n, A.thr4);
+      const bool k4 = n < N && (use_mw ? ((mw[u] >> 12) & 1u) != 0u
+                                       : sg_keep(pk, 4, side, (uint32_t)n, A.thr4));
       if (!BWD) {
         if (g == 0 && n < N)
           A.X[((int64_t)side * A.Cp + p) * A.Dp + n] = k4 ? z * A.ik4 : 0.f;
+        if (A.masks != nullptr && n < N)
+          A.masks[((size_t)q * A.Dp + n) * 4 + g] = (uint16_t)(mw[u] | (k4 ? 1u << 12 : 0u));
       } else {
         // Dense / Padding / NTN-input backward: gZ1 (= gH2, identity act) in registers
         const float gx = k4 ? sGxk[n] * A.ik4 : 0.f;
@@ -2051,6 +2100,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
   // those of the one-stream sequence (SG_WEB_PIPE=0).
   const char *pipe_e = getenv("SG_WEB_PIPE");   // read per call (a test toggles it)
   const bool pipe_env = !(pipe_e && pipe_e[0] == '0');
+
   hipStream_t gs = st;
   hipEvent_t evF = nullptr, evG[2] = {nullptr, nullptr};
   const int64_t nch = n_pairs > 0 ? (n_pairs + chunk - 1) / chunk : 0;
@@ -2060,6 +2110,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
   const bool pipe = gs != st;
   struct Slot {
     float *X, *GX, *T, *GM;
+    uint16_t *MASK;
     int2 *EXT, *EXT16, *EXT128;
     int4 *INST;
     int32_t *isort, *icnt, *icls;
@@ -2072,6 +2123,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     S.EXT128 = (int2 *)(sb + ws.EXT128); S.INST = (int4 *)(sb + ws.INST);
     S.isort = (int32_t *)(sb + ws.ISORT); S.icnt = (int32_t *)(sb + ws.ICNT);
     S.icls = (int32_t *)(sb + ws.ICLS);
+    S.MASK = (uint16_t *)(sb + ws.MASK);
     return S;
   };
   auto gcn_args = [&](int64_t c, const Slot &S) {
@@ -2082,6 +2134,8 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     g.isorted = units ? S.isort : nullptr;
     g.icls = units ? S.icls : nullptr;
     g.X = S.X;
+    // the forward's dropout bits for the backward (training calls)
+    g.masks = (bwd && SG_WEB_MASKS) ? S.MASK : nullptr;
     g.GX = S.GX;
     g.n_pairs = n;
     g.pair_offset = pair_offset + c0;
@@ -2101,7 +2155,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
       const int32_t *cp = pairs + 2 * c0;
       hipLaunchKernelGGL(web_icls_count, dim3(nbu), dim3(256), 0, st, S.INST, cp, 2 * n, cap4,
                          cap2, xparts, nbu, S.icnt);
-      hipLaunchKernelGGL(web_icls_scan, dim3(1), dim3(64), 0, st, S.icnt, nbu, 2 * n, xparts,
+      hipLaunchKernelGGL(web_icls_scan, dim3(1), dim3(kScanT), 0, st, S.icnt, nbu, 2 * n, xparts,
                          S.icls);
       hipLaunchKernelGGL(web_icls_scatter, dim3(nbu), dim3(256), 0, st, S.INST, cp, 2 * n, cap4,
                          cap2, xparts, nbu, (const int32_t *)S.icnt, S.isort);
