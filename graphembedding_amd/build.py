@@ -43,9 +43,11 @@ def _stale() -> bool:
 
 # per-source compiler options (A/B-measured): the fused AIDS700nef kernel schedules for
 # ILP (max-ilp: +1.2%; the capacity-32 kernel measured 0.8% slower with it), the
-# capacity-32 kernel with the AMDGPU register-pressure trackers (+0.5%)
+# capacity-32 kernel with the AMDGPU register-pressure trackers (+0.5%), the graph-store
+# (C5) kernels for ILP (+1.0%: 4.006 vs 3.965 M pairs/s, profiles/r03_c5ab/)
 SOURCE_FLAGS = {'sg_fast.hip': ['-mllvm', '-amdgpu-sched-strategy=max-ilp'],
-                'sg_fast32.hip': ['-mllvm', '-amdgpu-use-amdgpu-trackers']}
+                'sg_fast32.hip': ['-mllvm', '-amdgpu-use-amdgpu-trackers'],
+                'sg_web.hip': ['-mllvm', '-amdgpu-sched-strategy=max-ilp']}
 
 
 def build_hip(force: bool = False, verbose: bool = False, out: str = None, defines=()) -> str:
