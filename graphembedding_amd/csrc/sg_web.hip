@@ -144,6 +144,7 @@ struct WebWs {
   int64_t X, GX, T, GM, EXT, EXT16, EXT128, INST;
   int64_t ISORT, ICNT, ICLS;                         // instance units (web_icls_*)
   int64_t MASK;   // uint16 [2 Cp][Dp][4]: the forward's dropout keep bits per (instance, node, g)
+  int64_t D2;     // [2 Cp][Dp][16]: the forward's D2 = dropout(H2) per (instance, node)
   int64_t SLOT;                                      // floats per slot
   int64_t Wg, Wh, GWS, GVS, GSLAB, HSLABo, total;    // per-call buffers
   int gcn_blocks, head_blocks;
@@ -155,6 +156,18 @@ int head_blocks_for() { return 2 * sg_num_cus(); }
 #ifndef SG_WEB_T_BF3
 #define SG_WEB_T_BF3 1
 #endif
+
+// The backward instance kernel reads the dropout keep bits the forward wrote (GcnArgs::masks)
+// instead of re-hashing 13 elements per lane and tile; 0: it re-hashes (A/B)
+#ifndef SG_WEB_MASKS
+#define SG_WEB_MASKS 1
+#endif
+// ... and the forward's D2 = dropout(H2) rows (GcnArgs::d2) instead of recomputing Z1 = D1'·W1
+// and the H2 pass, which also drops two of the unit's barriers; 0: it recomputes (A/B)
+#ifndef SG_WEB_D2
+#define SG_WEB_D2 1
+#endif
+static_assert(!SG_WEB_D2 || SG_WEB_MASKS, "the D2 rows need the keep bits");
 
 WebWs web_ws(const WebPlan &W, int64_t chunk) {
   WebWs w;
@@ -176,6 +189,7 @@ WebWs web_ws(const WebPlan &W, int64_t chunk) {
   w.ICNT = take(kIKeys * ((2 * w.Cp + kUnitChunk - 1) / kUnitChunk));
   w.ICLS = take(kIKeys + 8);
   w.MASK = take(4 * w.Cp * Dp);     // 2 Cp x Dp x 4 uint16
+  w.D2 = SG_WEB_D2 ? take(32 * w.Cp * Dp) : 0;   // 2 Cp x Dp x 16
   w.SLOT = o;
   o += w.SLOT;                      // slot 1
   w.Wg = take(K * Dp * Dp);
@@ -428,6 +442,9 @@ struct GcnArgs {
   // forward writes them, the backward reads them instead of re-hashing.  Bits 4c + s: layer 1,
   // feature 16c + 4g + s; 8 + s: layer 2, feature 4g + s; 12: layer 4 (the node's NTN input)
   uint16_t *masks;
+  // [2 n_pairs][Dp][16] the forward's D2 = dropout(H2) of every node (or null): the backward
+  // reads its nodes' rows instead of recomputing Z1 and the H2 pass
+  float *d2;
   const float *GX;   // [2][Cp][Dp] ∂L/∂x (backward)
   float *slab;       // [gridDim.x][n_gcn] (backward, accumulated)
   uint32_t key, thr0, thr1, thr2, thr4;
@@ -484,11 +501,6 @@ __host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, int max_nnz, bool b
   return L;
 }
 
-// The backward instance kernel reads the dropout keep bits the forward wrote (GcnArgs::masks)
-// instead of re-hashing 13 elements per lane and tile; 0: it re-hashes (A/B)
-#ifndef SG_WEB_MASKS
-#define SG_WEB_MASKS 1
-#endif
 
 // Σ_e val[e] · f(col[e]) over one CSR row.  SG_WEB_ROWP = 0 (default): four neighbours'
 // loads in flight at a time, then the tail one entry at a time; SG_WEB_ROWP = w > 0: w
@@ -672,10 +684,14 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
     // latency overlaps the staging below), the forward builds them
     uint32_t mw[GCN_TPW];
     constexpr bool use_mw = BWD && SG_WEB_MASKS;   // sg_web_run passes masks then
+    constexpr bool use_d2 = BWD && SG_WEB_D2;      // ... and the D2 rows
+    f4 d2v[GCN_TPW];
 #pragma unroll
     for (int u = 0; u < GCN_TPW; ++u) {
       const int n = 16 * (lw + u * WPI) + i;
       mw[u] = (use_mw && n < N) ? (uint32_t)A.masks[((size_t)q * A.Dp + n) * 4 + g] : 0u;
+      d2v[u] = (use_d2 && n < N) ? *(const f4 *)(A.d2 + ((size_t)q * A.Dp + n) * 16 + 4 * g)
+                                 : f4{0.f, 0.f, 0.f, 0.f};
     }
     const int *rp;
     const ColT *cl;
@@ -742,19 +758,21 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
 #pragma unroll
         for (int s = 0; s < 8; ++s) h[s] = 0.f;
       }
-      f4 z = {0.f, 0.f, 0.f, 0.f};
+      if (!use_d2) {   // Z1 = D1'·W1 (the backward with D2 rows needs no Z1)
+        f4 z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+        for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) z = mfma4(h[4 * c + s], sW1[(16 * c + 4 * g + s) * WH2 + i], z);
+          for (int s = 0; s < 4; ++s) z = mfma4(h[4 * c + s], sW1[(16 * c + 4 * g + s) * WH2 + i], z);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sZ1k[(16 * t + 4 * g + r) * ZS + i] = z[r];
+        for (int r = 0; r < 4; ++r) sZ1k[(16 * t + 4 * g + r) * ZS + i] = z[r];
+      }
       if (BWD) {
         *(float4 *)(sD1k + n * DS + 4 * g) = make_float4(h[0], h[1], h[2], h[3]);
         *(float4 *)(sD1k + n * DS + 16 + 4 * g) = make_float4(h[4], h[5], h[6], h[7]);
       }
     }
-    __syncthreads();
+    if (!use_d2) __syncthreads();   // Z1 complete before the H2 pass gathers it
     if (qn >= 0) {   // lands during the rest of this unit
       const int ntn = NT / gszn;
       load_rows(qn, inn, tid - (w / (GW_ / gszn)) * ntn);
@@ -768,9 +786,15 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
       if (t >= ntile) break;
       const int n = 16 * t + i;
       float h2[4] = {0.f, 0.f, 0.f, 0.f};
-      if (n < N) {
+      if (use_d2) {   // D2 = dropout(H2) as the forward wrote it (k2 applied: k2 ? h2 : 0)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) h2[s] = d2v[u][s];
+      } else if (n < N) {
         const float4 b = *(const float4 *)(sb1 + 4 * g);
         h2[0] = b.x; h2[1] = b.y; h2[2] = b.z; h2[3] = b.w;
+#ifdef SG_WEB_ABL_NOH2   // timing ablation only (results invalid): the backward skips the H2 pass
+        if (!BWD)
+#endif
         csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
           const float4 zz = *(const float4 *)(sZ1k + mm * ZS + 4 * g);
           h2[0] = fmaf(v, zz.x, h2[0]); h2[1] = fmaf(v, zz.y, h2[1]);
@@ -793,6 +817,9 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
       if (!BWD) {
         if (g == 0 && n < N)
           A.X[((int64_t)side * A.Cp + p) * A.Dp + n] = k4 ? z * A.ik4 : 0.f;
+        if (A.d2 != nullptr && n < N)
+          *(f4 *)(A.d2 + ((size_t)q * A.Dp + n) * 16 + 4 * g) =
+              f4{k2[0] ? h2[0] : 0.f, k2[1] ? h2[1] : 0.f, k2[2] ? h2[2] : 0.f, k2[3] ? h2[3] : 0.f};
         if (A.masks != nullptr && n < N)
           A.masks[((size_t)q * A.Dp + n) * 4 + g] = (uint16_t)(mw[u] | (k4 ? 1u << 12 : 0u));
       } else {
@@ -820,7 +847,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
       gsz = gszn;
       continue;
     }
-    __syncthreads();   // every wave is done reading Z1: it becomes gZ1
+    if (!use_d2) __syncthreads();   // every wave is done reading Z1: it becomes gZ1
 #pragma unroll
     for (int u = 0; u < GCN_TPW; ++u) {
       const int t = lw + u * WPI;
@@ -2111,6 +2138,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
   struct Slot {
     float *X, *GX, *T, *GM;
     uint16_t *MASK;
+    float *D2;
     int2 *EXT, *EXT16, *EXT128;
     int4 *INST;
     int32_t *isort, *icnt, *icls;
@@ -2124,6 +2152,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     S.isort = (int32_t *)(sb + ws.ISORT); S.icnt = (int32_t *)(sb + ws.ICNT);
     S.icls = (int32_t *)(sb + ws.ICLS);
     S.MASK = (uint16_t *)(sb + ws.MASK);
+    S.D2 = sb + ws.D2;
     return S;
   };
   auto gcn_args = [&](int64_t c, const Slot &S) {
@@ -2136,6 +2165,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     g.X = S.X;
     // the forward's dropout bits for the backward (training calls)
     g.masks = (bwd && SG_WEB_MASKS) ? S.MASK : nullptr;
+    g.d2 = (bwd && SG_WEB_D2) ? S.D2 : nullptr;
     g.GX = S.GX;
     g.n_pairs = n;
     g.pair_offset = pair_offset + c0;
