@@ -1137,6 +1137,43 @@ __global__ void __launch_bounds__(256) web_t_kernel(const float *__restrict__ X2
 // of 8 consecutive rows fall on distinct banks), 60 KiB; 32-deep contraction chunks,
 // the next chunk's f32 operands prefetched into registers during the MFMAs.
 constexpr int B3K = 32, B3S = 40;   // contraction chunk, LDS row stride (bf16)
+
+// Block order of the pair-block GEMMs.  SG_WEB_GXCD = 1: a 1-D grid where the NT column
+// tiles of pair block pb (and, for T, each k, slowest) run on blocks L ≡ pb (mod 8), which
+// the dispatcher deals to one XCD, so that the pair block's x rows would come into that
+// XCD's L2 once for all its tiles.  Measured 3.82-3.84 against 4.21-4.22 M pairs/s on C5
+// (profiles/r03_c5ab/gemm_*), so the default is the (pair block, tile, k) grid.
+#ifndef SG_WEB_GXCD
+#define SG_WEB_GXCD 0
+#endif
+__device__ __forceinline__ void web_pb_tile(int NT, int G8, int &pb, int &tile, int &kk) {
+#if SG_WEB_GXCD
+  const int L = (int)blockIdx.x;
+  int rest = L >> 3;
+  tile = rest % NT;
+  rest /= NT;
+  pb = (rest % G8) * 8 + (L & 7);
+  kk = rest / G8;
+#else
+  pb = (int)blockIdx.x;
+  tile = (int)blockIdx.y;
+  kk = (int)blockIdx.z;
+#endif
+}
+static dim3 web_pb_grid(int64_t nblk, int NT, int K) {
+#if SG_WEB_GXCD
+  const int64_t G8 = (nblk + 7) / 8;
+  return dim3((unsigned)(G8 * NT * 8 * K));
+#else
+  return dim3((unsigned)nblk, (unsigned)NT, (unsigned)K);
+#endif
+}
+// gX1 / gX2 GEMMs: the contraction runs over (32-deep chunk, k) with k inner, so a chunk's
+// x rows are loaded once and rescaled by gm[p][k] for each k (SG_WEB_GX_KIN=0: k outer, the
+// chunk reloaded per k; 4.19-4.20 against 4.21-4.22 M pairs/s on C5)
+#ifndef SG_WEB_GX_KIN
+#define SG_WEB_GX_KIN 1
+#endif
 constexpr int B3PART = TB * B3S;    // bf16 per part plane
 
 __device__ __forceinline__ void b3_split_store(uint16_t *plane, int r, int c, float4 x) {
@@ -1160,9 +1197,12 @@ __global__ void __launch_bounds__(256) web_t_kernel_b3(const float *__restrict__
                                                        const float *__restrict__ X1) {
   __shared__ __attribute__((aligned(16))) uint16_t sA[3 * B3PART], sB[3 * B3PART];
   __shared__ float mred[2][TB];
-  const int64_t p0 = (int64_t)blockIdx.x * TB;
-  const int a0 = blockIdx.y * TB, k = blockIdx.z;
-  const int2 e = ext128[blockIdx.x];
+  int pbk, at, k;
+  web_pb_tile(Dp / TB, (int)((n + TB * 8 - 1) / (TB * 8)), pbk, at, k);
+  if ((int64_t)pbk * TB >= n) return;
+  const int64_t p0 = (int64_t)pbk * TB;
+  const int a0 = at * TB;
+  const int2 e = ext128[pbk];
   if (a0 >= e.x) return;
   const int nb = (e.y + B3K - 1) / B3K * B3K;   // x2 is zero past n2 (Dp is a multiple of 128)
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, i = l & 15, g = l >> 4;
@@ -1231,7 +1271,7 @@ __global__ void __launch_bounds__(256) web_t_kernel_b3(const float *__restrict__
       }
     __syncthreads();
     if (tid < TB && p0 + tid < n)
-      Tout[((p0 + tid) * WKP + k) * 4 + blockIdx.y] = mred[0][tid] + mred[1][tid];
+      Tout[((p0 + tid) * WKP + k) * 4 + at] = mred[0][tid] + mred[1][tid];
     return;
   }
 #pragma unroll
@@ -1311,22 +1351,25 @@ __global__ void __launch_bounds__(256) web_gx2_kernel_b3(const float *__restrict
                                                          int64_t n, int Dp, int K,
                                                          float *__restrict__ GX2) {
   __shared__ __attribute__((aligned(16))) uint16_t sA[3 * B3PART], sB[3 * B3PART];
-  const int64_t p0 = (int64_t)blockIdx.x * TB;
-  const int b0 = blockIdx.y * TB;
-  const int2 e = ext128[blockIdx.x];
+  int pb, bt, kk_;
+  web_pb_tile(Dp / TB, (int)((n + TB * 8 - 1) / (TB * 8)), pb, bt, kk_);
+  if ((int64_t)pb * TB >= n) return;
+  const int64_t p0 = (int64_t)pb * TB;
+  const int b0 = bt * TB;
+  const int2 e = ext128[pb];
   if (b0 >= e.y) return;
   const int na = (e.x + B3K - 1) / B3K * B3K;
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, i = l & 15, g = l >> 4;
   const int wm = w >> 1, wn = w & 1;
   float4 ra[4], rb[4];
   float gmr[4];
-  auto load = [&](int k, int a0) {
+  auto load = [&](int k, int a0, bool xload) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int q = tid + 256 * u, r = q >> 3, c = (q & 7) * 4;
       const int64_t p = p0 + r;
       gmr[u] = p < n ? GM[p * WKP + k] : 0.f;
-      ra[u] = *(const float4 *)(X1 + p * Dp + a0 + c);
+      if (xload) ra[u] = *(const float4 *)(X1 + p * Dp + a0 + c);
       rb[u] = *(const float4 *)(Wh + ((size_t)k * Dp + b0 + r) * Dp + a0 + c);
     }
   };
@@ -1336,7 +1379,7 @@ __global__ void __launch_bounds__(256) web_gx2_kernel_b3(const float *__restrict
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f4{0.f, 0.f, 0.f, 0.f};
   const int steps = na / B3K, total = K * steps;
-  if (total > 0) load(0, 0);
+  if (total > 0) load(0, 0, true);
   for (int st = 0; st < total; ++st) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -1346,7 +1389,11 @@ __global__ void __launch_bounds__(256) web_gx2_kernel_b3(const float *__restrict
       b3_split_store(sB, r, c, rb[u]);
     }
     __syncthreads();
-    if (st + 1 < total) load((st + 1) / steps, ((st + 1) % steps) * B3K);
+    if (st + 1 < total) {
+      const int s1 = st + 1;
+      if (SG_WEB_GX_KIN) load(s1 % K, (s1 / K) * B3K, s1 % K == 0);
+      else load(s1 / steps, (s1 % steps) * B3K, true);
+    }
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
       const int oa = (wm * 64 + mi * 16 + i) * B3S + 8 * g;
@@ -1474,22 +1521,25 @@ __global__ void __launch_bounds__(256) web_gx1_kernel_b3(const float *__restrict
                                                          int64_t n, int Dp, int K,
                                                          float *__restrict__ GX1) {
   __shared__ __attribute__((aligned(16))) uint16_t sA[3 * B3PART], sB[3 * B3PART];
-  const int64_t p0 = (int64_t)blockIdx.x * TB;
-  const int a0 = blockIdx.y * TB;
-  const int2 e = ext128[blockIdx.x];
+  int pb, at, kk_;
+  web_pb_tile(Dp / TB, (int)((n + TB * 8 - 1) / (TB * 8)), pb, at, kk_);
+  if ((int64_t)pb * TB >= n) return;
+  const int64_t p0 = (int64_t)pb * TB;
+  const int a0 = at * TB;
+  const int2 e = ext128[pb];
   if (a0 >= e.x) return;
   const int nb = (e.y + B3K - 1) / B3K * B3K;
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, i = l & 15, g = l >> 4;
   const int wm = w >> 1, wn = w & 1;
   float4 ra[4], rb[4];
   float gmr[4];
-  auto load = [&](int k, int b0) {
+  auto load = [&](int k, int b0, bool xload) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int q = tid + 256 * u, r = q >> 3, c = (q & 7) * 4;
       const int64_t p = p0 + r;
       gmr[u] = p < n ? GM[p * WKP + k] : 0.f;
-      ra[u] = *(const float4 *)(X2 + p * Dp + b0 + c);
+      if (xload) ra[u] = *(const float4 *)(X2 + p * Dp + b0 + c);
       rb[u] = *(const float4 *)(Wg + ((size_t)k * Dp + a0 + r) * Dp + b0 + c);
     }
   };
@@ -1499,7 +1549,7 @@ __global__ void __launch_bounds__(256) web_gx1_kernel_b3(const float *__restrict
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f4{0.f, 0.f, 0.f, 0.f};
   const int steps = nb / B3K, total = K * steps;
-  if (total > 0) load(0, 0);
+  if (total > 0) load(0, 0, true);
   for (int st = 0; st < total; ++st) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -1509,7 +1559,11 @@ __global__ void __launch_bounds__(256) web_gx1_kernel_b3(const float *__restrict
       b3_split_store(sB, r, c, rb[u]);
     }
     __syncthreads();
-    if (st + 1 < total) load((st + 1) / steps, ((st + 1) % steps) * B3K);
+    if (st + 1 < total) {
+      const int s1 = st + 1;
+      if (SG_WEB_GX_KIN) load(s1 % K, (s1 / K) * B3K, s1 % K == 0);
+      else load(s1 / steps, (s1 % steps) * B3K, true);
+    }
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
       const int oa = (wm * 64 + mi * 16 + i) * B3S + 8 * g;
@@ -2199,7 +2253,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     const int64_t nblk = (n + TB - 1) / TB;
     float *X = S.X, *GX = S.GX, *T = S.T, *GM = S.GM;
     if (SG_WEB_T_BF3)
-      hipLaunchKernelGGL(web_t_kernel_b3<true>, dim3((unsigned)nblk, Dp / TB, K), dim3(256), 0,
+      hipLaunchKernelGGL(web_t_kernel_b3<true>, web_pb_grid(nblk, Dp / TB, K), dim3(256), 0,
                          gs, X + ws.Cp * Dp, Wg, S.EXT128, n, Dp, K, T, X);
     else
       hipLaunchKernelGGL(web_t_kernel, dim3((unsigned)nblk, Dp / TB, K), dim3(256), 0, gs,
@@ -2213,9 +2267,9 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     if (bwd) {
       if (SG_WEB_T_BF3) {
         hipLaunchKernelGGL((web_head_kernel<true, true>), dim3(hb), dim3(256), head_lds, gs, h);
-        hipLaunchKernelGGL(web_gx1_kernel_b3, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, gs,
+        hipLaunchKernelGGL(web_gx1_kernel_b3, web_pb_grid(nblk, Dp / TB, 1), dim3(256), 0, gs,
                            X + ws.Cp * Dp, GM, Wg, S.EXT128, n, Dp, K, GX);
-        hipLaunchKernelGGL(web_gx2_kernel_b3, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, gs, X,
+        hipLaunchKernelGGL(web_gx2_kernel_b3, web_pb_grid(nblk, Dp / TB, 1), dim3(256), 0, gs, X,
                            GM, Wh, S.EXT128, n, Dp, K, GX + ws.Cp * Dp);
         // gV rides along
         hipLaunchKernelGGL(web_wgrad_kernel_b3, dim3((Dp / TB) * (Dp / TB), K, WSPLIT), dim3(256),
