@@ -48,7 +48,10 @@ constexpr int TB = 128;             // GEMM tile edge
 constexpr int MKS = 20;             // MK LDS tile row stride (16 + 4): conflict-free b128 reads
 constexpr int KMS = TB + 4;         // KM LDS tile row stride
 constexpr int HSLAB = 1 + 2 * WKP;  // head slab row: loss | gU[16] | gb[16]
-constexpr int WSPLIT = 8;           // split-K over pairs of the weight-gradient GEMMs
+#ifndef SG_WEB_WSPLIT
+#define SG_WEB_WSPLIT 16
+#endif
+constexpr int WSPLIT = SG_WEB_WSPLIT;   // split-K over pairs of the weight-gradient GEMMs
 constexpr int kUnitChunk = 4096;    // instances per block of the size-class sort (web_icls_*)
 // XCD partitions of the instance units: instances of graph g go to partition g % kXcdParts,
 // and unit slot u runs on the workgroups with blockIdx.x = u (mod kXcdParts), which the
@@ -1802,6 +1805,9 @@ struct HeadArgs {
   float yeta, inv_batch;
 };
 
+#ifndef SG_WEB_HEAD_TRIM
+#define SG_WEB_HEAD_TRIM 1
+#endif
 // MT: T holds web_t_kernel_b3<true>'s a-tile shares MP[p][k][tile] of Σ_a x1[a] T[k][a]
 // instead of T, and gx1 gets only its V term here (web_gx1_kernel_b3 adds the T term)
 template <bool BWD, bool MT>
@@ -1828,13 +1834,18 @@ __global__ void __launch_bounds__(256) web_head_kernel(HeadArgs A) {
   float aLoss = 0.f, aU = 0.f, aB = 0.f;   // lane k: gU[k], gb[k]
   const int64_t gw = (int64_t)blockIdx.x * 4 + w, nw = (int64_t)gridDim.x * 4;
   for (int64_t p = gw; p < A.n; p += nw) {
-    const int e1 = A.ext[p].x;
+    const int2 ex = A.ext[p];
+    const int e1 = ex.x;
+    // x1 / x2 are zero past the extents (padding 0) and gx past them is never read (the
+    // instance kernels take ∂L/∂x of present nodes only): 64-wide column blocks up to the
+    // larger extent (SG_WEB_HEAD_TRIM=0: all Dp / 64)
+    const int ncp = SG_WEB_HEAD_TRIM ? min(nc, (max(ex.x, ex.y) + 63) >> 6) : nc;
     const float *x1 = A.X + p * Dp, *x2 = A.X + (A.Cp + p) * Dp;
     const float *Tp = A.T + (size_t)p * K * Dp;
     float m[WKP];
 #pragma unroll
     for (int k = 0; k < WKP; ++k) m[k] = 0.f;
-    for (int c = 0; c < nc; ++c) {
+    for (int c = 0; c < ncp; ++c) {
       const int a = 64 * c + l;
       const float xa = x1[a], xb = x2[a];
 #pragma unroll
@@ -1901,7 +1912,7 @@ __global__ void __launch_bounds__(256) web_head_kernel(HeadArgs A) {
     }
     if (l == 0 && A.s_out) A.s_out[p] = s;
     float *g1 = A.GX + p * Dp, *g2 = A.GX + (A.Cp + p) * Dp;
-    for (int c = 0; c < nc; ++c) {
+    for (int c = 0; c < ncp; ++c) {
       const int a = 64 * c + l;
       float v1 = 0.f, v2 = 0.f;
 #pragma unroll
