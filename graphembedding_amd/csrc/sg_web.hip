@@ -422,6 +422,9 @@ __global__ void __launch_bounds__(256) web_wprep_h(const float *__restrict__ Wg,
 #ifndef SG_WEB_FWD_WAVES
 #define SG_WEB_FWD_WAVES 8
 #endif
+#ifndef SG_WEB_FWD_BPC_DEF
+#define SG_WEB_FWD_BPC_DEF 2
+#endif
 __host__ __device__ constexpr int gcn_gw(bool bwd) { return bwd ? SG_WEB_BWD_WAVES : SG_WEB_FWD_WAVES; }
 
 struct GcnArgs {
@@ -2050,9 +2053,14 @@ static int gcn_launch(bool bwd, const WebPlan &W, const GcnArgs &A, int64_t n_in
   if (lcsr) A_.isorted = nullptr, A_.icls = nullptr;   // LCSR stages one instance at a time
   int per_cu = (int)(163840u / lds);
   if (per_cu > 2048 / (64 * gcn_gw(bwd))) per_cu = 2048 / (64 * gcn_gw(bwd));
-  if (!bwd) {   // A/B: forward blocks per CU (room for the pipelined GEMMs beside them)
+  if (!bwd) {
+    // forward blocks per CU: 2 of the 3 that the LDS admits (4.445 vs 4.32 M pairs/s on C5,
+    // profiles/r03_c5ab/knob_*: fewer blocks contend for the CU's LDS and issue slots, and
+    // leave room for the pipelined GEMMs); SG_WEB_FWD_BPC=n sets it (A/B)
+    int want = SG_WEB_FWD_BPC_DEF;
     const char *e = getenv("SG_WEB_FWD_BPC");
-    if (e && atoi(e) > 0 && atoi(e) < per_cu) per_cu = atoi(e);
+    if (e && atoi(e) > 0) want = atoi(e);
+    if (want < per_cu) per_cu = want;
   }
   int64_t blocks = (int64_t)sg_num_cus() * per_cu;
   if (bwd) blocks = sg_num_cus();   // one slab row per block (web_ws sizes the slab for this)
