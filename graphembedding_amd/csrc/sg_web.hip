@@ -154,7 +154,10 @@ struct WebWs {
 };
 
 int gcn_blocks_for() { return sg_num_cus(); }
-int head_blocks_for() { return 2 * sg_num_cus(); }
+#ifndef SG_WEB_HEAD_BPC
+#define SG_WEB_HEAD_BPC 3
+#endif
+int head_blocks_for() { return SG_WEB_HEAD_BPC * sg_num_cus(); }
 
 #ifndef SG_WEB_T_BF3
 #define SG_WEB_T_BF3 1
@@ -2020,6 +2023,16 @@ int64_t sg_web_ws_bytes(const sg_model_t *m, int64_t chunk) {
   return web_ws(W, chunk).total * 4 + 256;
 }
 
+// A/B: dynamic LDS padding of a GEMM launch (bytes, from the environment), which lowers the
+// blocks a CU holds at once (the GEMMs hold ≈61-67 KB of static LDS: 2 blocks per CU)
+static size_t web_lds_pad(const char *name, const void *fn) {
+  const char *e = getenv(name);
+  const int v = e ? atoi(e) : 0;
+  if (v <= 0) return 0;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, v);
+  return (size_t)v;
+}
+
 static int web_status() {
   const hipError_t e = hipGetLastError();
   if (e == hipSuccess) return SG_OK;
@@ -2272,8 +2285,9 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     const int64_t nblk = (n + TB - 1) / TB;
     float *X = S.X, *GX = S.GX, *T = S.T, *GM = S.GM;
     if (SG_WEB_T_BF3)
-      hipLaunchKernelGGL(web_t_kernel_b3<true>, web_pb_grid(nblk, Dp / TB, K), dim3(256), 0,
-                         gs, X + ws.Cp * Dp, Wg, S.EXT128, n, Dp, K, T, X);
+      hipLaunchKernelGGL(web_t_kernel_b3<true>, web_pb_grid(nblk, Dp / TB, K), dim3(256),
+                         web_lds_pad("SG_WEB_TPAD", (const void *)web_t_kernel_b3<true>), gs,
+                         X + ws.Cp * Dp, Wg, S.EXT128, n, Dp, K, T, X);
     else
       hipLaunchKernelGGL(web_t_kernel, dim3((unsigned)nblk, Dp / TB, K), dim3(256), 0, gs,
                          X + ws.Cp * Dp, Wg, S.EXT128, n, Dp, K, T);
@@ -2286,13 +2300,16 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     if (bwd) {
       if (SG_WEB_T_BF3) {
         hipLaunchKernelGGL((web_head_kernel<true, true>), dim3(hb), dim3(256), head_lds, gs, h);
-        hipLaunchKernelGGL(web_gx1_kernel_b3, web_pb_grid(nblk, Dp / TB, 1), dim3(256), 0, gs,
+        hipLaunchKernelGGL(web_gx1_kernel_b3, web_pb_grid(nblk, Dp / TB, 1), dim3(256),
+                           web_lds_pad("SG_WEB_GXPAD", (const void *)web_gx1_kernel_b3), gs,
                            X + ws.Cp * Dp, GM, Wg, S.EXT128, n, Dp, K, GX);
-        hipLaunchKernelGGL(web_gx2_kernel_b3, web_pb_grid(nblk, Dp / TB, 1), dim3(256), 0, gs, X,
+        hipLaunchKernelGGL(web_gx2_kernel_b3, web_pb_grid(nblk, Dp / TB, 1), dim3(256),
+                           web_lds_pad("SG_WEB_GXPAD", (const void *)web_gx2_kernel_b3), gs, X,
                            GM, Wh, S.EXT128, n, Dp, K, GX + ws.Cp * Dp);
         // gV rides along
         hipLaunchKernelGGL(web_wgrad_kernel_b3, dim3((Dp / TB) * (Dp / TB), K, WSPLIT), dim3(256),
-                           0, gs, X, X + ws.Cp * Dp, GM, S.EXT16, n, Dp, K, GWS, GVS);
+                           web_lds_pad("SG_WEB_WGPAD", (const void *)web_wgrad_kernel_b3), gs, X,
+                           X + ws.Cp * Dp, GM, S.EXT16, n, Dp, K, GWS, GVS);
       } else {
         hipLaunchKernelGGL((web_head_kernel<true, false>), dim3(hb), dim3(256), head_lds, gs, h);
         hipLaunchKernelGGL(web_gx2_kernel, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, gs, X, GM,
