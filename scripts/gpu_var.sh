@@ -1,6 +1,6 @@
 #!/bin/bash
-# Bench A/B over variants, alternating over REPS rounds.  A variant is NAME=ENV1,ENV2,...
-# (environment assignments such as SG_LIB=graphembedding_amd/lib/x.so; "base=" for none).
+# Bench A/B over variants, alternating over REPS rounds.  A variant is NAME=ENV1+ENV2+...
+# (environment assignments joined by '+', such as SG_LIB=graphembedding_amd/lib/x.so; "base=" for none).
 # BENCH_ARGS: the bench.py flags (default: the driver's command, --gpus 1 --steps 20
 # --warmup 5).  TESTS (optional): pytest targets run first, with TEST_ENV applied.
 # Usage: scripts/gpu_var.sh TAG variant...
@@ -20,7 +20,7 @@ ARGS=${BENCH_ARGS:---gpus 1 --steps 20 --warmup 5}
 for rep in $(seq 1 ${REPS:-2}); do
   for v in "$@"; do
     n=${v%%=*}; e=${v#*=}
-    envs=$(echo "$e" | tr ',' ' ')
+    envs=$(echo "$e" | tr '+' ' ')
     env $envs timeout -k 10 300 python bench.py $ARGS --cpu-sample -1 \
       --json-out "$OUT/${n}_$rep.json" > "$OUT/${n}_$rep.log" 2>&1
     r=$?
