@@ -250,6 +250,9 @@ def main():
                     why), file=sys.stderr, flush=True)
                 collective = 'torch'
             else:
+                if comm.device() != local:   # open_rccl's init thread must select our GPU
+                    raise RuntimeError('RCCL communicator on GPU {} for local rank {}'.format(
+                        comm.device(), local))
                 hook = make_rccl_hook(comm)
         if collective == 'torch':
             hook = make_allreduce_hook()

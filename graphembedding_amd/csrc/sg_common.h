@@ -7,6 +7,15 @@
 
 #define SG_WAVE 64
 
+// Timing ablations (scripts/gpu_abl_*.sh) remove work and give WRONG results.  They
+// compile only together with SG_TIMING_ABLATION_BUILD, which build.py never passes to
+// the product library (graphembedding_amd/lib/libsiamese_hip.so), so a hand build
+// with one ablation macro alone fails here instead of producing a silently wrong .so.
+#if (defined(SG32_ABL_NOREC) || defined(SG32_ABL_NONTN) || defined(SG_WEB_ABL_NOH2)) && \
+    !defined(SG_TIMING_ABLATION_BUILD)
+#error "timing ablation macro without SG_TIMING_ABLATION_BUILD: results would be invalid"
+#endif
+
 // ---------------------------------------------------------------------------
 // Counter-based dropout RNG.  Bit-exact twin of oracle/siamese_oracle.py
 // (sg_mix, seed_key, dropout_mask).  Replaces TF's unseeded

@@ -1323,6 +1323,20 @@ int sg_ntn_wgrad_run(const float *ntn, int64_t n_pairs, int D, int oW, int oV, i
 
 int sg_fast_needs_ntn(const SgGenPlan &P) { return plan_avg(P) ? 1 : 0; }
 
+struct ClassWeights {
+  float w[4];
+};
+
+static ClassWeights class_weights_from_env() {
+  ClassWeights c = {{1.f, 1.29f, 1.31f, 1.47f}};
+  if (const char *ev = getenv("SG_CLS_W")) {
+    float w[4];
+    if (sscanf(ev, "%f,%f,%f,%f", &w[0], &w[1], &w[2], &w[3]) == 4)
+      for (int k = 0; k < 4; ++k) c.w[k] = w[k] > 0.f ? w[k] : 1.f;
+  }
+  return c;
+}
+
 int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
                 const int32_t *order, int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
                 uint64_t seed, const float *y_stats, float *s_out, float *slab, float *ntn,
@@ -1350,14 +1364,12 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
   // relative cost of a pair of class (N0 > 8) + 2 (N1 > 8): the class-exclusive schedule
   // gives each class waves in proportion to count x cost (SG_CLS_W="w0,w1,w2,w3" to tune)
   // (measured per-class µs/pair, scripts/fast_timing.py, profiles/r03_tim: 1, 1.29, 1.31, 1.47)
-  A.cw[0] = 1.f;
-  A.cw[1] = 1.29f;
-  A.cw[2] = 1.31f;
-  A.cw[3] = 1.47f;
-  if (const char *ev = getenv("SG_CLS_W")) {
-    float w[4];
-    if (sscanf(ev, "%f,%f,%f,%f", &w[0], &w[1], &w[2], &w[3]) == 4)
-      for (int k = 0; k < 4; ++k) A.cw[k] = w[k] > 0.f ? w[k] : 1.f;
+  // (the environment is parsed once per process, and only for class-scheduled launches)
+  if (A.cls) {
+    static const ClassWeights cwt = class_weights_from_env();
+    for (int k = 0; k < 4; ++k) A.cw[k] = cwt.w[k];
+  } else {
+    for (int k = 0; k < 4; ++k) A.cw[k] = 1.f;
   }
   A.n_pairs = n_pairs;
   A.rw4h = P.hbm_words / 4;

@@ -51,6 +51,7 @@ def _rccl():
                                     ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.ncclCommDestroy.argtypes = [ctypes.c_void_p]
         L.ncclCommAbort.argtypes = [ctypes.c_void_p]
+        L.ncclCommCuDevice.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
         L.ncclGetErrorString.argtypes = [ctypes.c_int]
         L.ncclGetErrorString.restype = ctypes.c_char_p
     return _LIB
@@ -112,6 +113,12 @@ class RcclComm(object):
         p = t.data_ptr()
         _check(_rccl().ncclAllReduce(p, p, t.numel(), NCCL_FLOAT32, NCCL_SUM, self.comm,
                                      ctypes.c_void_p(int(stream))), 'ncclAllReduce')
+
+    def device(self) -> int:
+        """The GPU the communicator was initialised on (ncclCommCuDevice)."""
+        d = ctypes.c_int(-1)
+        _check(_rccl().ncclCommCuDevice(self.comm, ctypes.byref(d)), 'ncclCommCuDevice')
+        return int(d.value)
 
     def destroy(self):
         if self.comm:
@@ -189,9 +196,23 @@ def open_rccl(rank: int, world: int, store=None, group=None, timeout_s: float = 
         return None, reason or 'a peer rank could not load RCCL or get the unique id'
 
     box = {}
+    # HIP keeps the current device per host thread and a new thread starts on device 0:
+    # the helper thread must select this rank's GPU before ncclCommInitRank, or every rank
+    # would initialise its communicator on GPU 0
+    dev = None
+    try:
+        import torch
+        if torch.cuda.is_available():
+            dev = torch.cuda.current_device()
+    except Exception:   # noqa: BLE001 (CPU-only callers: gloo tests with fake init)
+        dev = None
+    box['device'] = dev
 
     def init():
         try:
+            if dev is not None:
+                import torch
+                torch.cuda.set_device(dev)
             if _init is not None:
                 box['comm'] = _init(lib, raw, rank, world)
                 return

@@ -95,9 +95,13 @@ def test(data, dist_calculator, model, flags=None, evaluator=None, verbose=True)
                                        batch_total=m * n)
                 _sync()
                 t = _time.time()
-                model.test_scores(one)
+                s1 = model.test_scores(one)
                 _sync()
                 time_mat[i][j] = (_time.time() - t) * 1000.0
+                if s1[0] != s[i * n + j]:   # same keys, same kernel: bit-identical
+                    raise RuntimeError('per_pair score ({}, {}) = {!r} differs from the batched '
+                                       'score {!r}'.format(i, j, float(s1[0]),
+                                                           float(s[i * n + j])))
     elif time_mode == 'batched':
         time_mat = np.full((m, n), elapsed * 1000.0 / max(1, m * n))   # msec per pair
     else:

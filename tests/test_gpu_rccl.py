@@ -66,6 +66,7 @@ def test_rccl_direct_world1_hook_keeps_step_bitwise(gpu):
     batches = [shard.batch(m) for m in models]
     comm = RcclComm(0, 1, store=dist.HashStore())
     try:
+        assert comm.device() == torch.cuda.current_device()
         hook = make_rccl_hook(comm)
         for _ in range(3):
             for k, (m, b) in enumerate(zip(models, batches)):
@@ -93,6 +94,8 @@ def _two_rank_worker(rank, world, port, q):
         from graphembedding_amd.rccl import open_rccl
         comm, why = open_rccl(rank, world)
         assert comm is not None, why
+        # the init runs on a helper thread, which must have selected this rank's GPU
+        assert comm.device() == rank, (rank, comm.device())
         n = 2727   # an odd count: a wrong count or datatype enum would show
         g = torch.Generator().manual_seed(100 + rank)
         x = torch.randn(n, generator=g, dtype=torch.float32).to(dev)

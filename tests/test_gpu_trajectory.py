@@ -13,6 +13,9 @@ equals the host get_feed_dict byte for byte, each step's loss (incl. weight deca
 powers) within 2e-5 of the oracle's update from that state, and the free-running
 parameters after 20 steps within 1e-4 of the free-running float64 oracle — which pins the
 float32 β-power progression, weight decay across steps and the sampler's wraps.
+After every train step the validation leg (train.py:19-21,88-93: the loss on a val feed,
+no update) is checked too: device val feed == host val feed, val loss within 1e-4 of the
+oracle at the post-step parameters with the val seed stream's masks.
 Dropout 0 and 0.1."""
 import numpy as np
 import pytest
@@ -71,7 +74,14 @@ def test_default_loop_20_steps_match_oracle(gpu, dropout):
     flat = p0.astype(np.float64)
     st = O.adam_init(flat.size)
     W = record_words(model.n_max, model.record_dtype)
-    steps, worst = [], 0.0
+    # the validation leg of train_val (train.py:19-21,88-93): sess.run([loss]) on a val
+    # feed after every train step — the loss at the current parameters, no update, with
+    # dropout masks from the val seed stream; fed by the device val feed, which must equal
+    # the host get_feed_dict(..., 'val') byte for byte
+    from graphembedding_amd.device_sampler import DeviceFeed
+    data_v, dc_v = make()
+    vfeed = DeviceFeed(model, data_v, dc_v, 'val')
+    steps, worst, vworst = [], 0.0, 0.0
     for step in range(STEPS):
         b = feed.next_batch()
         words = b.records.cpu().numpy().view(np.uint32).reshape(b.n_pairs, W).copy()
@@ -98,13 +108,31 @@ def test_default_loop_20_steps_match_oracle(gpu, dropout):
         assert one <= 2e-5, (step, one)
         assert abs(loss - r1.loss) <= 1e-4 * max(1.0, abs(r1.loss)), (step, loss, r1.loss)
         steps.append((loss, res.loss))
+        # validation: device val feed == host val feed; loss vs the oracle at 1e-4
+        vb = vfeed.next_batch()
+        vwords = vb.records.cpu().numpy().view(np.uint32).reshape(vb.n_pairs, W).copy()
+        hv = model.get_feed_dict(data_h, dc_h, 'val')
+        assert np.array_equal(hv.records.cpu().numpy().view(np.uint32).reshape(-1, W),
+                              vwords), ('val feed', step)
+        assert np.array_equal(hv.labels.cpu().numpy(), vb.labels.cpu().numpy()), ('val', step)
+        vseed = model.val_seed()
+        g_before = model.grad_loss.clone()
+        vloss = model.val_loss(vb)
+        assert torch.equal(g_before, model.grad_loss), 'val_loss must not touch grad | loss'
+        v1, v2 = _oracle_graphs(vwords, model.n_max)
+        rv = O.fwd_bwd(spec, model.params.cpu().numpy().astype(np.float64), v1, v2,
+                       vb.labels.cpu().numpy().astype(np.float64), vseed)
+        verr = abs(vloss - rv.loss) / max(1.0, abs(rv.loss))
+        vworst = max(vworst, verr)
+        assert verr <= 1e-4, ('val loss', step, vloss, rv.loss)
     feed.sampler.sync_host()   # the reference's in-place list shuffle (A6), after 20 steps
     assert [g.nxgraph.graph['gid'] for g in data_h.train_data.gs] == \
         [g.nxgraph.graph['gid'] for g in feed.sampler.host.gs]
     got = model.params.cpu().numpy().astype(np.float64)
     err = float(np.abs(got - flat).max())
     print('dropout {}: per-step (teacher-forced) max |param err| {:.3g}; free-running 20-step '
-          'max |param err| {:.3g}; losses (gpu, oracle) {}'.format(dropout, worst, err, steps))
+          'max |param err| {:.3g}; worst val-loss rel err {:.3g}; losses (gpu, oracle) {}'.format(
+              dropout, worst, err, vworst, steps))
     # free-running float32 vs float64 trajectories drift apart: Adam's first steps move a
     # parameter by ~lr·sign(g) whatever |g| is, so rounding-level differences of the
     # smallest gradient components grow across steps (measured: 9.3e-6 at dropout 0,

@@ -118,3 +118,21 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, '_lib', None)
     with pytest.raises(_lib.SiameseHipError, match='no CPU fallback'):
         _lib.lib()
+
+
+@pytest.mark.parametrize('macro', ['SG32_ABL_NOREC', 'SG32_ABL_NONTN', 'SG_WEB_ABL_NOH2'])
+def test_timing_ablation_macro_alone_does_not_compile(macro):
+    """A timing ablation (results invalid) compiles only with SG_TIMING_ABLATION_BUILD
+    also set (sg_common.h #error), so a hand build cannot yield a silently wrong .so."""
+    import subprocess
+    hipcc = '/opt/rocm/bin/hipcc'
+    if not os.path.isfile(hipcc):
+        pytest.skip('no hipcc')
+    hdr = os.path.join(ROOT, 'graphembedding_amd', 'csrc', 'sg_common.h')
+    base = [hipcc, '--offload-arch=gfx950', '-std=c++17', '-E', '-x', 'hip', hdr, '-o',
+            os.devnull]
+    bad = subprocess.run(base + ['-D' + macro], capture_output=True, text=True)
+    assert bad.returncode != 0 and 'timing ablation' in bad.stderr
+    ok = subprocess.run(base + ['-D' + macro, '-DSG_TIMING_ABLATION_BUILD'],
+                        capture_output=True, text=True)
+    assert ok.returncode == 0, ok.stderr[-2000:]
