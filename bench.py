@@ -57,9 +57,10 @@ def parse():
                    help='C4 streamed from the store: pairs per launch')
     p.add_argument('--resident-gb', type=float, default=150.0,
                    help='C4: keep a shard\'s records resident up to this many GB')
-    p.add_argument('--stack', choices=('default', 'average'), default='default',
-                   help="layer stack: the default config.py:44-66 stack, or tuning.py:66-93's "
-                        "GCN-GCN-Average-NTN(16)")
+    p.add_argument('--stack', choices=('default', 'average', 'attention'), default='default',
+                   help="layer stack: the default config.py:44-66 stack, tuning.py:66-93's "
+                        "GCN-GCN-Average-NTN(16), or the same with Attention pooling "
+                        "(layers.py:143-160)")
     p.add_argument('--collective', choices=('rccl', 'torch'), default='rccl',
                    help='N > 1: the gradient all-reduce as ncclAllReduce on the compute stream '
                         '(rccl) or through torch.distributed (side stream + events)')
@@ -191,8 +192,9 @@ def main():
         fl.update(layer_3='Padding:max_in_dims=30,padding_value=0',
                   layer_4='NTN:input_dim=30,feature_map_dim=10,inneract=relu,dropout=True,'
                           'bias=True')
-    if args.stack == 'average':   # the tuning.py stack (layers_factory.py Average + NTN(16))
-        fl.update(num_layers=4, layer_2='Average',
+    if args.stack in ('average', 'attention'):   # the tuning.py stack (Average + NTN(16))
+        fl.update(num_layers=4,
+                  layer_2='Average' if args.stack == 'average' else 'Attention:input_dim=16',
                   layer_3='NTN:input_dim=16,feature_map_dim=10,inneract=relu,dropout=True,'
                           'bias=True')
     if web:   # Web: N <= 512 needs Padding / NTN input_dim 512
@@ -330,7 +332,7 @@ def main():
 
     if rank == 0:
         flops_pair = gs.flops_per_pair_web() if web else gs.flops_per_pair(
-            D=D, pool='average' if args.stack == 'average' else 'padding')
+            D=D, pool={'default': 'padding'}.get(args.stack, args.stack))
         bytes_pair = gs.csr_bytes_per_pair() if web else shard.record_bytes
         kern_pairs_s = shard.n / (kern_ms * 1e-3)
         achieved_tf = kern_pairs_s * flops_pair / 1e12
@@ -400,8 +402,10 @@ def main():
             'data': 'synthetic ({}-shaped graphs + GED labels, BASELINE.md §3)'.format(
                 'Web' if web else ('AIDS10knef' if c4 else 'AIDS700nef')),
             'config': {'workload': workload +
-                                   (', default 5-layer Siamese GCN-NTN' if args.stack == 'default' else
-                                    ', tuning.py GCN-GCN-Average-NTN(16) stack') +
+                                   {'default': ', default 5-layer Siamese GCN-NTN',
+                                    'average': ', tuning.py GCN-GCN-Average-NTN(16) stack',
+                                    'attention': ', GCN-GCN-Attention(16)-NTN(16) stack '
+                                                 '(layers.py:143-160)'}[args.stack] +
                                    ', dropout {}'.format(args.dropout),
                        'global_batch': total_pairs, 'n_max': gs.n_max, 'd_in': gs.d_in,
                        'kernel_path': _lib.PATH_NAMES[model.kernel_path],

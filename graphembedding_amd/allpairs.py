@@ -62,11 +62,20 @@ class GraphSet:
     def flops_per_pair(self, h1=32, h2=16, D=10, K=10, pool='padding') -> float:
         """Algorithmic FLOPs per pair, fwd+bwd (SURVEY §8(d) formula), averaged
         over the all-pairs stream (every graph is g1 G times and g2 G times).
-        pool='average': the tuning.py stack (no Dense; mean over nodes, NTN D = h2)."""
+        pool='average': the tuning.py stack (no Dense; mean over nodes, NTN D = h2);
+        pool='attention': the same with Attention pooling (layers.py:143-160)."""
         n = np.array([g.number_of_nodes() for g in self.graphs], dtype=np.float64)
         e = np.array([g.number_of_edges() for g in self.graphs], dtype=np.float64)
         nnz = n + 2 * e
-        head_f, head_b = (2 * n * h2, 4 * n * h2) if pool == 'padding' else (n * h2, n * h2)
+        if pool == 'padding':
+            head_f, head_b = 2 * n * h2, 4 * n * h2
+        elif pool == 'attention':
+            # layers.py:154-160: mean n h2, h = tanh(temp Wa) 2 h2², att = σ(H2 h) 2 n h2,
+            # attᵀ H2 2 n h2; backward gatt and gh 2 n h2 each, gWa and gtemp 2 h2² each,
+            # ∂H2 = att gout + gz h + gtemp / n 4 n h2
+            head_f, head_b = 5 * n * h2 + 2 * h2 * h2, 8 * n * h2 + 4 * h2 * h2
+        else:
+            head_f, head_b = n * h2, n * h2
         if pool != 'padding':
             D = h2
         fwd = 2 * h1 * n + 2 * h1 * nnz + 2 * n * h1 * h2 + 2 * h2 * nnz + head_f

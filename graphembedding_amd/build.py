@@ -8,7 +8,7 @@ import sys
 _HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(_HERE, 'csrc')
 OUT = os.path.join(_HERE, 'lib', 'libsiamese_hip.so')
-SOURCES = ['siamese_hip.hip', 'sg_generic.hip', 'sg_fast.hip', 'sg_fast32.hip',
+SOURCES = ['siamese_hip.hip', 'sg_generic.hip', 'sg_fast.hip', 'sg_fast_att.hip', 'sg_fast32.hip',
            'sg_sampler.hip', 'sg_web.hip']
 HEADERS = ['sg_common.h', 'sg_plan.h', 'sg_mfma.h']
 # MI355X only: the kernels use gfx950's 160 KB LDS (web_wgrad_kernel_b3 holds ≈66.6 KB),
@@ -46,6 +46,7 @@ def _stale() -> bool:
 # capacity-32 kernel with the AMDGPU register-pressure trackers (+0.5%), the graph-store
 # (C5) kernels for ILP (+1.0%: 4.006 vs 3.965 M pairs/s, profiles/r03_c5ab/)
 SOURCE_FLAGS = {'sg_fast.hip': ['-mllvm', '-amdgpu-sched-strategy=max-ilp'],
+                'sg_fast_att.hip': ['-mllvm', '-amdgpu-sched-strategy=max-ilp'],
                 'sg_fast32.hip': ['-mllvm', '-amdgpu-use-amdgpu-trackers'],
                 'sg_web.hip': ['-mllvm', '-amdgpu-sched-strategy=max-ilp']}
 

@@ -100,6 +100,7 @@ struct FastArgs {
   int d_in, n_params;
   int shared_floats, wave_floats;
   int oW0, ob0, oW1, ob1, oWd, obd, oW, oV, oU, obn;
+  int oWa;   // Attention weights (ATT), -1 otherwise
   // pair source (sg_pair_source_t): src_store = 1 gathers each record from the dense
   // graph store instead of reading a packed one
   int src_store, G;
@@ -155,7 +156,11 @@ __device__ __forceinline__ uint4 fast_store_word(const FastArgs &A, int p, int w
   return uint4{v[0], v[1], v[2], v[3]};
 }
 
-template <int D, bool AVG = false>
+// Attention pooling (ATT, with AVG = true: the 16-feature pooled head): the 16x16
+// weight table at row stride 17 (conflict-free row and column reads)
+constexpr int WAS = 17;
+
+template <int D, bool AVG = false, bool ATT = false>
 struct FastLds {
   // NTN width DN (the Padding width D, or H2's 16 features after Average), the row
   // stride WR of the NTN W tables and VS of the V table
@@ -168,26 +173,28 @@ struct FastLds {
   static constexpr int TILE = REC + RW;               // 2 x 16 x TS1 (D1 tiles)
   static constexpr int X = TILE + 2 * 16 * TS1;       // x1 | x2 (at 12, or 16 for AVG); [47] = 0
   static constexpr int GE = X + 48;                   // AVG: ∂L/∂x1 | ∂L/∂x2 (16 each)
-  static int wave_floats(int) { return X + 48 + (AVG ? 32 : 0); }
+  static constexpr int TMP = GE + 32;                 // ATT: node means of H2 (16 per side)
+  static constexpr int GU = TMP + 32;                 // ATT: ∂L/∂(tanh input) (16 per side)
+  static int wave_floats(int) { return X + 48 + (AVG ? 32 : 0) + (ATT ? 64 : 0); }
   static int shared_floats(int d_in) {
     return (d_in + 1) * FH1 + 2 * DN * FK * WR + FK * VS + FH1 * W1S + FH2 * W1TS +
-           (SG_GD1_BF16 ? 2 * 3 * 64 * 4 : 0);
+           (SG_GD1_BF16 ? 2 * 3 * 64 * 4 : 0) + (ATT ? FH2 * WAS : 0);
   }
 };
 
 
 // Flush slots of one lane: gW1 (8) | gW0/ik0 (16) | NTN dW (RN·DN) | dV (RN + RN) |
-// dbn, dU, loss | db0 (2), db1, dWd, dbd (pre-summed over row groups)
-template <int D, bool AVG = false>
+// dbn, dU, loss | db0 (2), db1, dWd, dbd (pre-summed over row groups) | ATT: gWa (4)
+template <int D, bool AVG = false, bool ATT = false>
 struct FlushSlots {
   static constexpr int DN = FastLds<D, AVG>::DN, RN = (DN + 3) / 4;
   // AVG: the NTN W, V and bias gradients go through the per-pair buffer instead
   static constexpr int NWS = AVG ? 0 : RN * DN, NVS = AVG ? 0 : 2 * RN;
-  static constexpr int NS = 8 + 16 + NWS + NVS + 3 + 5;
+  static constexpr int NS = 8 + 16 + NWS + NVS + 3 + 5 + (ATT ? 4 : 0);
 };
 
 // parameter index of slot s on lane l = 16 g + j, or -1 if the slot is padding
-template <int D, bool AVG>
+template <int D, bool AVG, bool ATT>
 __device__ __forceinline__ int fast_param(const FastArgs &A, int s, int l) {
   constexpr int DN = FastLds<D, AVG>::DN, RN = (DN + 3) / 4;
   constexpr int NWS = FlushSlots<D, AVG>::NWS, NVS = FlushSlots<D, AVG>::NVS;
@@ -218,8 +225,20 @@ __device__ __forceinline__ int fast_param(const FastArgs &A, int s, int l) {
     case 5: return g == 0 ? A.ob1 + j : -1;
     case 6: return (!AVG && g == 0) ? A.oWd + j : -1;
     case 7: return (!AVG && l == 0) ? A.obd : -1;
-    default: return -1;
+    default: break;
   }
+  s -= 8;
+  // ATT: lane (g, j) slot i holds gWa[4i + g][j] (Attention weights [input_dim][input_dim])
+  return (ATT && s < 4) ? A.oWa + (4 * s + g) * FH2 + j : -1;
+}
+
+// tanh and the logistic function from v_exp_f32 and v_rcp_f32 (≈1e-7 relative; the
+// Attention layer's h and att, layers.py:156-157)
+__device__ __forceinline__ float sg_tanh(float z) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * z) + 1.f);
+}
+__device__ __forceinline__ float sg_sigmoid(float z) {
+  return __builtin_amdgcn_rcpf(1.f + __expf(-z));
 }
 
 #ifdef SG_FAST_TIMING
@@ -237,11 +256,12 @@ __device__ unsigned long long sg_fast_times[kTimeWaves * 5];
 #define SG_STAMP(slot, val) do {} while (0)
 #endif
 
-template <int D, bool BWD, bool ALIGNED, bool INTENDED, bool AVG, bool SRC>
+template <int D, bool BWD, bool ALIGNED, bool INTENDED, bool AVG, bool SRC, bool ATT>
 __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
+  static_assert(!ATT || AVG, "Attention pooling uses the 16-feature pooled head");
   SG_STAMP(0, __builtin_amdgcn_s_memrealtime());
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  using L = FastLds<D, AVG>;
+  using L = FastLds<D, AVG, ATT>;
   constexpr int DN = L::DN, RN = (DN + 3) / 4, WR = L::WR, VS = L::VS;
   constexpr int XO2 = AVG ? 16 : 12;       // x2 offset in the wave's x region
   constexpr uint32_t NL = AVG ? 3u : 4u;   // layer index of the NTN (its dropout key)
@@ -371,6 +391,8 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   // [t][term][lane] bf16 B operands of gD1 (SG_GD1_BF16): lane (g, j) ↔ column 16t + j,
   // k-slots 8g..8g+3 / 8g+4..8g+7 ↔ parts of W1[16t + j][4g..4g+3]·ik1
   uint4 *sW1B = (uint4 *)(sW1T + FH2 * W1TS);
+  // ATT: Attention weights Wa[j'][k] at row stride WAS
+  float *sWat = SG_GD1_BF16 ? (float *)(sW1B + 2 * 3 * 64) : sW1T + FH2 * W1TS;
   float *W = smem + A.shared_floats + wv * A.wave_floats;
   float *sRec = W + L::REC;
   float *sT = W + L::TILE;
@@ -432,6 +454,8 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
                         : (term == 1 ? uint4{m01, m23, h01, h23} : uint4{l01, l23, m01, m23});
   }
 #endif
+  if constexpr (ATT)
+    for (int i = tid; i < FH2 * FH2; i += blockDim.x) sWat[(i >> 4) * WAS + (i & 15)] = stg[A.oWa + i];
   // per-lane parameters, also from the staged copy
   const int j_ = tid & 15;
   const float b0v0 = stg[A.ob0 + j_] * A.ik1, b0v1 = stg[A.ob0 + 16 + j_] * A.ik1;
@@ -504,6 +528,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
     for (int b = 0; b < (DW_ + 1) / 2; ++b) gWn[r][b] = f2{0.f, 0.f};
   }
   float gbn = 0.f, gUa = 0.f, lossa = 0.f;
+  float gwa[4] = {0.f, 0.f, 0.f, 0.f};   // ATT: gWa[4i + g][j]
   const float ybar = (BWD && !ALIGNED) ? A.y_stats[0] : 0.f;
 
   // Waves w and w ^ 4 share a SIMD (round-robin placement).  Issue arbitration
@@ -725,7 +750,62 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       // uses it as the whole mask of the Dense/Padding/dropout chain.
       float xo[2][RN], d2[2][3];
       uint32_t kb = 0u;   // layer-2 keep bits, bit 3s + r
-      if constexpr (AVG) {
+      float hA[2] = {0.f, 0.f};                             // ATT: h_s[j]
+      float att[2][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};  // ATT: att of node 4r + g
+      if constexpr (ATT) {
+        // Attention (layers.py:154-160): temp = mean of the node rows of H2, h = tanh(temp
+        // Wa), att_n = sigmoid(H2[n] · h), e = Σ_n att_n H2[n]; x_s[j] = keep · e_j · ik4.
+        // Lane (g, j) holds H2 rows 4r + g at feature j; absent rows (b1) are masked.
+        float *sTmp = W + L::TMP;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int KS = s2 ? K1 : K0, Ns = s2 ? N1 : N0;
+          float part = 0.f;
+#pragma unroll
+          for (int r = 0; r < KS; ++r) part += (4 * r + g < Ns) ? h2[s2][r] : 0.f;
+          const float e = xsum32(xsum16(part)) * (s2 ? invn1 : invn0);
+          if (g == 0) sTmp[16 * s2 + j] = e;
+        }
+        sg_wsync();
+        float hp[2];   // row group g: the terms j' = 4g..4g+3 of (temp · Wa)[j]
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          float a = 0.f;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            a = fmaf(sTmp[16 * s2 + 4 * g + i], sWat[(4 * g + i) * WAS + j], a);
+          hp[s2] = a;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) hA[s2] = sg_tanh(xsum32(xsum16(hp[s2])));
+        float dd[K0 + K1];   // H2[n] · h: the node rows' sums, both sides interleaved
+#pragma unroll
+        for (int r = 0; r < K0; ++r) dd[r] = h2[0][r] * hA[0];
+#pragma unroll
+        for (int r = 0; r < K1; ++r) dd[K0 + r] = h2[1][r] * hA[1];
+        row_sum16_n(dd);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int KS = s2 ? K1 : K0, Ns = s2 ? N1 : N0;
+          float po = 0.f;
+#pragma unroll
+          for (int r = 0; r < KS; ++r) {
+            const float a = sg_sigmoid(dd[s2 * K0 + r]);
+            att[s2][r] = a;
+            po += (4 * r + g < Ns) ? a * h2[s2][r] : 0.f;
+          }
+          const float e = xsum32(xsum16(po));
+          const bool k4 = (m4 >> (16 * s2 + j)) & 1u;
+          if (g == 0) sX[XO2 * s2 + j] = k4 ? e * A.ik4 : 0.f;
+        }
+        sg_wsync();
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int r = 0; r < RN; ++r) xo[s2][r] = sX[XO2 * s2 + 4 * r + g];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) d2[0][r] = d2[1][r] = 0.f;
+      } else if constexpr (AVG) {
         // x_s[j] = keep · mean over the side's nodes of H2[·][j] · ik4 (layers.py:136-140,
         // 287-288): lane (g, j) holds the rows of nodes 4r + g; absent rows hold b1
 #pragma unroll
@@ -905,7 +985,8 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       // ================= GCN backward =================
       f4 gh2[2], gz1t[2];
       float dq[2][2][3];   // [side][t][q]: this lane's D1 entries
-      float gej[2] = {0.f, 0.f};   // AVG: ∂L/∂e_s[j] / N_s
+      float gej[2] = {0.f, 0.f};   // AVG: ∂L/∂e_s[j] / N_s;  ATT: ∂L/∂e_s[j]
+      float gxa[2][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};   // ATT: ∂L/∂H2 of node 4r + g
       if constexpr (AVG) {
         // ∂L/∂x of element a = 4r + g (equal on a row's 16 lanes) → by feature j
         float *sGE = W + L::GE;
@@ -917,8 +998,59 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           }
         }
         sg_wsync();
-        gej[0] = ((m4 >> j) & 1u) ? sGE[j] * invn0 : 0.f;
-        gej[1] = ((m4 >> (16 + j)) & 1u) ? sGE[16 + j] * invn1 : 0.f;
+        gej[0] = ((m4 >> j) & 1u) ? sGE[j] * (ATT ? 1.f : invn0) : 0.f;
+        gej[1] = ((m4 >> (16 + j)) & 1u) ? sGE[16 + j] * (ATT ? 1.f : invn1) : 0.f;
+      }
+      if constexpr (ATT) {
+        // Attention backward (adjoint of layers.py:154-160, oracle _node_backward):
+        //   gatt_n = gout · H2[n],  gz_n = gatt_n att_n (1 - att_n),  gh = Σ_n gz_n H2[n],
+        //   gu = gh (1 - h²),  gWa += temp ⊗ gu,  gtemp = Wa gu,
+        //   ∂L/∂H2[n] = att_n gout + gz_n h + gtemp / N
+        float *sTmp = W + L::TMP, *sGU = W + L::GU;
+        float ga[K0 + K1];
+#pragma unroll
+        for (int r = 0; r < K0; ++r) ga[r] = gej[0] * h2[0][r];
+#pragma unroll
+        for (int r = 0; r < K1; ++r) ga[K0 + r] = gej[1] * h2[1][r];
+        row_sum16_n(ga);
+        float ghp[2] = {0.f, 0.f}, gz[2][3];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int KS = s2 ? K1 : K0, Ns = s2 ? N1 : N0;
+#pragma unroll
+          for (int r = 0; r < KS; ++r) {
+            const float a = att[s2][r];
+            const float z = (4 * r + g < Ns) ? ga[s2 * K0 + r] * (a * (1.f - a)) : 0.f;
+            gz[s2][r] = z;
+            ghp[s2] = fmaf(z, h2[s2][r], ghp[s2]);
+          }
+        }
+        float gu[2];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const float gh = xsum32(xsum16(ghp[s2]));
+          gu[s2] = gh * (1.f - hA[s2] * hA[s2]);
+          if (g == 0) sGU[16 * s2 + j] = gu[s2];
+        }
+        sg_wsync();
+        float gtp[2];   // row group g: the terms k = 4g..4g+3 of (Wa gu)[j]
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) gwa[i] = fmaf(sTmp[16 * s2 + 4 * i + g], gu[s2], gwa[i]);
+          float a = 0.f;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a = fmaf(sGU[16 * s2 + 4 * g + i], sWat[j * WAS + 4 * g + i], a);
+          gtp[s2] = a;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int KS = s2 ? K1 : K0;
+          const float gt = xsum32(xsum16(gtp[s2])) * (s2 ? invn1 : invn0);
+#pragma unroll
+          for (int r = 0; r < KS; ++r)
+            gxa[s2][r] = fmaf(att[s2][r], gej[s2], fmaf(gz[s2][r], hA[s2], gt));
+        }
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -926,8 +1058,8 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         gh2[s] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int r = 0; r < KS; ++r) {
-          if constexpr (AVG) {   // mean: every present node gets ∂L/∂e / N
-            const float v = (4 * r + g < (s ? N1 : N0)) ? gej[s] : 0.f;
+          if constexpr (AVG) {   // mean: every present node gets ∂L/∂e / N (ATT: gxa)
+            const float v = (4 * r + g < (s ? N1 : N0)) ? (ATT ? gxa[s][r] : gej[s]) : 0.f;
             gb1a += v;
             gh2[s][r] = v;
           } else {
@@ -1107,7 +1239,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   // every parameter is hit exactly once, so the slab row is written directly.
   // Waves are summed in fixed order (deterministic).  The block owns the CU's
   // LDS (one block per CU), so all its waves' slots fit (fast_cfg).
-  constexpr int NS = FlushSlots<D, AVG>::NS;
+  constexpr int NS = FlushSlots<D, AVG, ATT>::NS;
   {
     // per-feature bias / Dense gradients: sum the four row groups in registers
     gb0a0 = xsum32(xsum16(gb0a0));
@@ -1149,11 +1281,15 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
     Fw[64 * s++] = gb1a;
     Fw[64 * s++] = gwda;
     Fw[64 * s++] = gbda;
+    if constexpr (ATT) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Fw[64 * s++] = gwa[i];
+    }
   }
   __syncthreads();
   float *dst = A.slab + (size_t)blockIdx.x * (size_t)(A.n_params + 1);
   for (int idx = tid; idx < NS * 64; idx += blockDim.x) {
-    const int prm_i = fast_param<D, AVG>(A, idx >> 6, idx & 63);
+    const int prm_i = fast_param<D, AVG, ATT>(A, idx >> 6, idx & 63);
     if (prm_i < 0) continue;
     float acc = 0.f;
     for (int w = 0; w < nw; ++w) acc += F[(size_t)w * NS * 64 + idx];
@@ -1170,12 +1306,14 @@ struct FastCfg {
   int shared_floats, wave_floats;
 };
 
-template <int D, bool AVG>
+template <int D, bool AVG, bool ATT>
 FastCfg fast_cfg_t(int d_in, int n_params, int64_t n_pairs, bool bwd) {
   FastCfg c;
   c.D = D;
-  c.shared_floats = FastLds<D, AVG>::shared_floats(d_in);
-  c.wave_floats = FastLds<D, AVG>::wave_floats(d_in);
+  using LL = FastLds<D, AVG, ATT>;
+  using FS = FlushSlots<D, AVG, ATT>;
+  c.shared_floats = LL::shared_floats(d_in);
+  c.wave_floats = LL::wave_floats(d_in);
   // resident waves per CU allowed by registers: the backward kernel uses up to
   // 256 VGPRs (2 waves / SIMD), the forward-only one ~120 (4 waves / SIMD)
   const int wcap = bwd ? MAXW : 2 * MAXW;
@@ -1187,7 +1325,7 @@ FastCfg fast_cfg_t(int d_in, int n_params, int64_t n_pairs, bool bwd) {
     if (force > 0 && nw != force) continue;
     const size_t lds = (size_t)(c.shared_floats + nw * c.wave_floats) * 4u;
     if (lds > 163840u) break;
-    if (bwd && (size_t)nw * FlushSlots<D, AVG>::NS * 256u > 163840u) break;   // flush slots fit
+    if (bwd && (size_t)nw * FS::NS * 256u > 163840u) break;   // flush slots fit
     int per_cu = (int)(163840u / lds);
     int res = per_cu * nw;
     if (res > wcap) res = wcap;  // register-limited occupancy
@@ -1204,7 +1342,7 @@ FastCfg fast_cfg_t(int d_in, int n_params, int64_t n_pairs, bool bwd) {
   if (per_cu > wcap / best) per_cu = wcap / best;
   if (per_cu < 1) per_cu = 1;
   // the flush dumps every wave's accumulator slots into the block's LDS
-  const size_t fl = bwd ? (size_t)best * FlushSlots<D, AVG>::NS * 64u * 4u : 0u;
+  const size_t fl = bwd ? (size_t)best * FS::NS * 64u * 4u : 0u;
   // the prologue stages the parameter vector behind the shared tables
   const size_t stage = (size_t)(c.shared_floats + n_params) * 4u;
   const size_t need = fl > stage ? fl : stage;
@@ -1218,11 +1356,45 @@ FastCfg fast_cfg_t(int d_in, int n_params, int64_t n_pairs, bool bwd) {
   return c;
 }
 
+template <int D, bool BWD, bool ALIGNED, bool INTENDED, bool AVG, bool SRC, bool ATT>
+void launch_one(const FastCfg &c, const FastArgs &A, hipStream_t st) {
+  const void *fn = (const void *)sg_fast_kernel<D, BWD, ALIGNED, INTENDED, AVG, SRC, ATT>;
+  if (c.lds > 65536u)
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds);
+  hipLaunchKernelGGL((sg_fast_kernel<D, BWD, ALIGNED, INTENDED, AVG, SRC, ATT>), dim3(c.blocks),
+                     dim3(64 * c.waves), c.lds, st, A);
+}
+
+template <int D, bool AVG, bool SRC, bool ATT>
+void launch_fast_src(const FastCfg &c, bool bwd, bool aligned, bool intended,
+                     const FastArgs &A, hipStream_t st) {
+  if (!bwd) {
+    if (intended) launch_one<D, false, false, true, AVG, SRC, ATT>(c, A, st);
+    else launch_one<D, false, false, false, AVG, SRC, ATT>(c, A, st);
+  } else if (aligned) {
+    if (intended) launch_one<D, true, true, true, AVG, SRC, ATT>(c, A, st);
+    else launch_one<D, true, true, false, AVG, SRC, ATT>(c, A, st);
+  } else {
+    if (intended) launch_one<D, true, false, true, AVG, SRC, ATT>(c, A, st);
+    else launch_one<D, true, false, false, AVG, SRC, ATT>(c, A, st);
+  }
+}
+
+// SRC: store-sourced pairs (a separate instantiation: the gather's registers would
+// otherwise cost the record path spills)
+template <int D, bool AVG, bool ATT = false>
+void launch_fast(const FastCfg &c, bool bwd, bool aligned, bool intended,
+                 const FastArgs &A, hipStream_t st) {
+  if (A.src_store) launch_fast_src<D, AVG, true, ATT>(c, bwd, aligned, intended, A, st);
+  else launch_fast_src<D, AVG, false, ATT>(c, bwd, aligned, intended, A, st);
+}
+
 }  // namespace
 
 // --------------------------------------------------------------------------
-// tuning.py:66-93 stack: GCN(d_in→32, relu) → GCN(32→16) → Average → NTN(16, K=10)
-static bool fast_avg_shape(const sg_model_t *m, const SgGenPlan &P) {
+// Pooled-head stacks (tuning.py:66-93): GCN(d_in→32, relu) → GCN(32→16) → Average or
+// Attention(16) (layers.py:121-160) → NTN(16, K=10)
+static bool fast_pool_shape(const sg_model_t *m, const SgGenPlan &P) {
   if (m->num_layers != 4) return false;
   const sg_layer_t *Ly = m->layers;
   if (Ly[0].kind != SG_GCN || !Ly[0].sparse_inputs || Ly[0].output_dim != FH1 ||
@@ -1231,7 +1403,8 @@ static bool fast_avg_shape(const sg_model_t *m, const SgGenPlan &P) {
   if (Ly[1].kind != SG_GCN || Ly[1].input_dim != FH1 || Ly[1].output_dim != FH2 ||
       Ly[1].act != SG_ACT_IDENTITY || !Ly[1].bias)
     return false;
-  if (Ly[2].kind != SG_AVERAGE) return false;
+  if (Ly[2].kind != SG_AVERAGE && !(Ly[2].kind == SG_ATTENTION && Ly[2].input_dim == FH2))
+    return false;
   if (Ly[3].kind != SG_NTN || Ly[3].input_dim != FH2 || Ly[3].output_dim != FK ||
       Ly[3].act != SG_ACT_RELU || !Ly[3].bias)
     return false;
@@ -1242,7 +1415,7 @@ static bool fast_avg_shape(const sg_model_t *m, const SgGenPlan &P) {
 }
 
 static bool fast_shape(const sg_model_t *m, const SgGenPlan &P) {
-  if (fast_avg_shape(m, P)) return true;
+  if (fast_pool_shape(m, P)) return true;
   if (m->num_layers != 5) return false;
   const sg_layer_t *Ly = m->layers;
   if (Ly[0].kind != SG_GCN || !Ly[0].sparse_inputs || Ly[0].output_dim != FH1 ||
@@ -1265,63 +1438,22 @@ static bool fast_shape(const sg_model_t *m, const SgGenPlan &P) {
   return P.n_params > 0;
 }
 
-int sg_fast_supported(const sg_model_t *m, const SgGenPlan &P) {
-  if (getenv("SG_DISABLE_FAST")) return 0;
-  return fast_shape(m, P) ? 1 : 0;
+// the pooled 16-feature head (Average or Attention: no Dense / Padding, NTN at layer 3)
+static bool plan_avg(const SgGenPlan &P) {
+  return P.nl == 3 && (P.L[2].kind == SG_AVERAGE || P.L[2].kind == SG_ATTENTION);
 }
-
-static bool plan_avg(const SgGenPlan &P) { return P.nl == 3 && P.L[2].kind == SG_AVERAGE; }
+static bool plan_att(const SgGenPlan &P) { return P.nl == 3 && P.L[2].kind == SG_ATTENTION; }
 
 static FastCfg fast_cfg(const SgGenPlan &P, int64_t n_pairs, bool bwd) {
+  if (plan_att(P))
+    return P.n_max == 12 ? fast_cfg_t<12, true, true>(P.d_in, P.n_params, n_pairs, bwd)
+                         : fast_cfg_t<10, true, true>(P.d_in, P.n_params, n_pairs, bwd);
   if (plan_avg(P))
-    return P.n_max == 12 ? fast_cfg_t<12, true>(P.d_in, P.n_params, n_pairs, bwd)
-                         : fast_cfg_t<10, true>(P.d_in, P.n_params, n_pairs, bwd);
-  return P.n_max == 12 ? fast_cfg_t<12, false>(P.d_in, P.n_params, n_pairs, bwd)
-                       : fast_cfg_t<10, false>(P.d_in, P.n_params, n_pairs, bwd);
+    return P.n_max == 12 ? fast_cfg_t<12, true, false>(P.d_in, P.n_params, n_pairs, bwd)
+                         : fast_cfg_t<10, true, false>(P.d_in, P.n_params, n_pairs, bwd);
+  return P.n_max == 12 ? fast_cfg_t<12, false, false>(P.d_in, P.n_params, n_pairs, bwd)
+                       : fast_cfg_t<10, false, false>(P.d_in, P.n_params, n_pairs, bwd);
 }
-
-int64_t sg_fast_slab_floats(const SgGenPlan &P, int64_t n_pairs) {
-  FastCfg c = fast_cfg(P, n_pairs, true);
-  return (int64_t)c.blocks * (P.n_params + 1);
-}
-
-template <int D, bool BWD, bool ALIGNED, bool INTENDED, bool AVG, bool SRC>
-static void launch_one(const FastCfg &c, const FastArgs &A, hipStream_t st) {
-  const void *fn = (const void *)sg_fast_kernel<D, BWD, ALIGNED, INTENDED, AVG, SRC>;
-  if (c.lds > 65536u)
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c.lds);
-  hipLaunchKernelGGL((sg_fast_kernel<D, BWD, ALIGNED, INTENDED, AVG, SRC>), dim3(c.blocks),
-                     dim3(64 * c.waves), c.lds, st, A);
-}
-
-template <int D, bool AVG, bool SRC>
-static void launch_fast_src(const FastCfg &c, bool bwd, bool aligned, bool intended,
-                            const FastArgs &A, hipStream_t st) {
-  if (!bwd) {
-    if (intended) launch_one<D, false, false, true, AVG, SRC>(c, A, st);
-    else launch_one<D, false, false, false, AVG, SRC>(c, A, st);
-  } else if (aligned) {
-    if (intended) launch_one<D, true, true, true, AVG, SRC>(c, A, st);
-    else launch_one<D, true, true, false, AVG, SRC>(c, A, st);
-  } else {
-    if (intended) launch_one<D, true, false, true, AVG, SRC>(c, A, st);
-    else launch_one<D, true, false, false, AVG, SRC>(c, A, st);
-  }
-}
-
-// SRC: store-sourced pairs (a separate instantiation: the gather's registers would
-// otherwise cost the record path spills)
-template <int D, bool AVG>
-static void launch_fast(const FastCfg &c, bool bwd, bool aligned, bool intended,
-                        const FastArgs &A, hipStream_t st) {
-  if (A.src_store) launch_fast_src<D, AVG, true>(c, bwd, aligned, intended, A, st);
-  else launch_fast_src<D, AVG, false>(c, bwd, aligned, intended, A, st);
-}
-
-int sg_ntn_wgrad_run(const float *ntn, int64_t n_pairs, int D, int oW, int oV, int obn, int C,
-                     float *slab, int blocks, hipStream_t st);
-
-int sg_fast_needs_ntn(const SgGenPlan &P) { return plan_avg(P) ? 1 : 0; }
 
 struct ClassWeights {
   float w[4];
@@ -1337,11 +1469,18 @@ static ClassWeights class_weights_from_env() {
   return c;
 }
 
-int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
-                const int32_t *order, int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
-                uint64_t seed, const float *y_stats, float *s_out, float *slab, float *ntn,
-                int *blocks_out, hipStream_t stream, const uint64_t *seed_dev,
-                const sg_pair_source_t *src, const int32_t *class_start) {
+int sg_ntn_wgrad_run(const float *ntn, int64_t n_pairs, int D, int oW, int oV, int obn, int C,
+                     float *slab, int blocks, hipStream_t st);
+
+// The host side of sg_fast_run.  The translation unit sg_fast_att.hip compiles this file
+// again with SG_FAST_ATT_TU defined and instantiates only the Attention kernels (the
+// default TU instantiates the rest): the two compile in parallel.
+static int fast_run_impl(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
+                         const int32_t *order, int64_t n_pairs, int64_t pair_offset,
+                         int64_t batch_total, const float *params, uint64_t seed,
+                         const float *y_stats, float *s_out, float *slab, float *ntn,
+                         int *blocks_out, hipStream_t stream, const uint64_t *seed_dev,
+                         const sg_pair_source_t *src, const int32_t *class_start) {
   const int D = P.n_max;
   FastCfg c = fast_cfg(P, n_pairs, bwd);
   // the kernel indexes pairs in 32 bits (2^31 records would be ≥ 1 TB)
@@ -1383,7 +1522,8 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
   A.key = sg_seed_key(seed);
   A.seed_dev = seed_dev;
   const float keep = m->keep_prob;
-  const bool avg = plan_avg(P);   // NTN is layer 3 after Average (no Dense / Padding)
+  const bool avg = plan_avg(P);   // NTN is layer 3 after Average / Attention
+  const bool att = plan_att(P);
   const float k0 = m->layers[0].dropout ? keep : 1.f, k1 = m->layers[1].dropout ? keep : 1.f;
   const float k2 = (!avg && m->layers[2].dropout) ? keep : 1.f;
   const float k4 = m->layers[avg ? 3 : 4].dropout ? keep : 1.f;
@@ -1407,30 +1547,83 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
   A.ob1 = P.L[1].offB;
   A.oWd = avg ? -1 : P.L[2].offW;
   A.obd = avg ? -1 : P.L[2].offB;
+  A.oWa = att ? P.L[2].offW : -1;
   A.oW = P.offW;
   A.oV = P.offV;
   A.oU = P.offU;
   A.obn = P.offB;
   const bool aligned = m->loss_mode == SG_LOSS_ALIGNED;
   const bool intended = m->ntn_mode == SG_NTN_INTENDED;
+  if (avg && bwd && !ntn) return SG_ERR_ARG;
+#ifdef SG_FAST_ATT_TU
+  if (!att) return SG_ERR_UNSUPPORTED;
+  if (D == 12) launch_fast<12, true, true>(c, bwd, aligned, intended, A, stream);
+  else launch_fast<10, true, true>(c, bwd, aligned, intended, A, stream);
+#else
+  if (att) return SG_ERR_UNSUPPORTED;   // sg_fast_att.hip
   if (avg) {
-    if (bwd && !ntn) return SG_ERR_ARG;
     if (D == 12) launch_fast<12, true>(c, bwd, aligned, intended, A, stream);
     else launch_fast<10, true>(c, bwd, aligned, intended, A, stream);
-    if (bwd) {
-      const int rc = sg_ntn_wgrad_run(ntn, n_pairs, FH2, P.offW, P.offV, P.offB, P.n_params + 1,
-                                      slab, c.blocks, stream);
-      if (rc != SG_OK) return rc;
-    }
   } else {
     if (D == 12) launch_fast<12, false>(c, bwd, aligned, intended, A, stream);
     else launch_fast<10, false>(c, bwd, aligned, intended, A, stream);
+  }
+#endif
+  if (avg && bwd) {   // the NTN W / V / bias gradients from the per-pair buffer
+    const int rc = sg_ntn_wgrad_run(ntn, n_pairs, FH2, P.offW, P.offV, P.offB, P.n_params + 1,
+                                    slab, c.blocks, stream);
+    if (rc != SG_OK) return rc;
   }
   if (blocks_out) *blocks_out = c.blocks;
   return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
 }
 
-#ifdef SG_FAST_TIMING
+#ifdef SG_FAST_ATT_TU
+int sg_fast_att_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
+                    const int32_t *order, int64_t n_pairs, int64_t pair_offset,
+                    int64_t batch_total, const float *params, uint64_t seed,
+                    const float *y_stats, float *s_out, float *slab, float *ntn, int *blocks_out,
+                    hipStream_t stream, const uint64_t *seed_dev, const sg_pair_source_t *src,
+                    const int32_t *class_start) {
+  return fast_run_impl(m, P, bwd, recs, order, n_pairs, pair_offset, batch_total, params, seed,
+                       y_stats, s_out, slab, ntn, blocks_out, stream, seed_dev, src, class_start);
+}
+#else
+int sg_fast_att_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
+                    const int32_t *order, int64_t n_pairs, int64_t pair_offset,
+                    int64_t batch_total, const float *params, uint64_t seed,
+                    const float *y_stats, float *s_out, float *slab, float *ntn, int *blocks_out,
+                    hipStream_t stream, const uint64_t *seed_dev, const sg_pair_source_t *src,
+                    const int32_t *class_start);
+
+int sg_fast_supported(const sg_model_t *m, const SgGenPlan &P) {
+  if (getenv("SG_DISABLE_FAST")) return 0;
+  return fast_shape(m, P) ? 1 : 0;
+}
+
+int64_t sg_fast_slab_floats(const SgGenPlan &P, int64_t n_pairs) {
+  FastCfg c = fast_cfg(P, n_pairs, true);
+  return (int64_t)c.blocks * (P.n_params + 1);
+}
+
+int sg_fast_needs_ntn(const SgGenPlan &P) { return plan_avg(P) ? 1 : 0; }
+
+int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
+                const int32_t *order, int64_t n_pairs, int64_t pair_offset, int64_t batch_total,
+                const float *params, uint64_t seed, const float *y_stats, float *s_out,
+                float *slab, float *ntn, int *blocks_out, hipStream_t stream,
+                const uint64_t *seed_dev, const sg_pair_source_t *src,
+                const int32_t *class_start) {
+  if (plan_att(P))
+    return sg_fast_att_run(m, P, bwd, recs, order, n_pairs, pair_offset, batch_total, params,
+                           seed, y_stats, s_out, slab, ntn, blocks_out, stream, seed_dev, src,
+                           class_start);
+  return fast_run_impl(m, P, bwd, recs, order, n_pairs, pair_offset, batch_total, params, seed,
+                       y_stats, s_out, slab, ntn, blocks_out, stream, seed_dev, src, class_start);
+}
+#endif
+
+#if defined(SG_FAST_TIMING) && !defined(SG_FAST_ATT_TU)
 extern "C" int sg_fast_timing_fetch(unsigned long long *host, int n) {
   if (n > kTimeWaves * 5) n = kTimeWaves * 5;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(sg_fast_times), (size_t)n * 8u, 0,

@@ -27,10 +27,12 @@ def _expected_order(prob, fused):
 
 
 @pytest.mark.parametrize('name,fused', [('default', True), ('average', True),
-                                        ('attention', False), ('default_bf16', True)])
+                                        ('attention', True), ('dot', False),
+                                        ('default_bf16', True)])
 def test_pair_order_is_stable_class_sort(gpu, name, fused):
     ov = {'default': {}, 'average': AVERAGE_STACK, 'default_bf16': dict(record_dtype='bf16'),
-          'attention': dict(AVERAGE_STACK, layer_2='Attention:input_dim=16')}[name]
+          'attention': dict(AVERAGE_STACK, layer_2='Attention:input_dim=16'),
+          'dot': dict(num_layers=5, layer_4='Dot')}[name]
     # > 2 sort chunks (8192 records), ragged last chunk, 1..10-node graphs
     prob = small_problem(n_graphs=50, n_pairs=20011, seed=31, n_lo=1, n_hi=10,
                          flags_overrides=ov)
@@ -41,10 +43,11 @@ def test_pair_order_is_stable_class_sort(gpu, name, fused):
     assert np.array_equal(got, _expected_order(prob, fused))
 
 
-@pytest.mark.parametrize('name', ['default', 'average', 'default_bf16'])
+@pytest.mark.parametrize('name', ['default', 'average', 'attention', 'default_bf16'])
 def test_ordered_step_equals_batch_order(gpu, name):
     import torch
-    ov = {'default': {}, 'average': AVERAGE_STACK, 'default_bf16': dict(record_dtype='bf16')}[name]
+    ov = {'default': {}, 'average': AVERAGE_STACK, 'default_bf16': dict(record_dtype='bf16'),
+          'attention': dict(AVERAGE_STACK, layer_2='Attention:input_dim=16')}[name]
     prob = small_problem(n_graphs=48, n_pairs=5000, seed=12, n_lo=2, n_hi=10,
                          flags_overrides=ov)
     model, batch = prob.make_gpu_model(device=gpu)
@@ -153,7 +156,7 @@ def test_class_schedule_equals_mixed_schedule(gpu, n_pairs):
 def test_class_table_needs_the_fused_path(gpu):
     """sg_pair_order_cls is the fused path's (path 1); other paths keep the plain order."""
     prob = small_problem(n_graphs=12, n_pairs=200, seed=5,
-                         flags_overrides=dict(AVERAGE_STACK, layer_2='Attention:input_dim=16'))
+                         flags_overrides=dict(num_layers=5, layer_4='Dot'))
     model, batch = prob.make_gpu_model(device=gpu)
     assert model.kernel_path == 0
     model.balance(batch)

@@ -16,6 +16,11 @@ STACKS = {
     'default_nodrop': dict(dropout=0.0),
     'average': AVERAGE_STACK,
     'attention': dict(AVERAGE_STACK, layer_2='Attention:input_dim=16'),
+    'attention_nodrop': dict(AVERAGE_STACK, layer_2='Attention:input_dim=16', dropout=0.0),
+    'attention_intended_aligned': dict(AVERAGE_STACK, layer_2='Attention:input_dim=16',
+                                       ntn_mode='intended', loss_mode='aligned'),
+    'attention_bf16_records': dict(AVERAGE_STACK, layer_2='Attention:input_dim=16',
+                                   record_dtype='bf16'),
     'dot': dict(num_layers=5, layer_4='Dot'),
     'dense_after_pad': dict(num_layers=6,
                             layer_3='Padding:max_in_dims=10,padding_value=0',
@@ -139,13 +144,13 @@ def test_nmax30_aids10k_shape(gpu):
     _check_grad(model.grad.cpu().numpy(), ref.grad_mse, prob)
 
 
-@pytest.mark.parametrize('stack', ['default', 'average'])
+@pytest.mark.parametrize('stack', ['default', 'average', 'attention'])
 def test_fast_path_matches_generic_path(gpu, monkeypatch, stack):
-    """The fused MFMA kernel and the generic LDS kernel agree on the default and
-    the tuning.py Average stacks (dropout on) — the generic path is the on-GPU
-    cross-check."""
+    """The fused MFMA kernel and the generic LDS kernel agree on the default, the
+    tuning.py Average and the Attention-pooling stacks (dropout on) — the generic path
+    is the on-GPU cross-check."""
     prob = small_problem(n_graphs=40, n_pairs=2000, seed=17,
-                         flags_overrides=AVERAGE_STACK if stack == 'average' else None)
+                         flags_overrides=None if stack == 'default' else STACKS[stack])
     model, batch = prob.make_gpu_model(device=gpu)
     assert model.kernel_path == 1, 'the stack must take the fused path'
     seed = 99
@@ -163,12 +168,14 @@ def test_fast_path_matches_generic_path(gpu, monkeypatch, stack):
 
 
 @pytest.mark.parametrize('case', ['one_type', 'types_32', 'nmax12', 'heavy_dropout',
-                                  'self_and_repeated_pairs'])
+                                  'self_and_repeated_pairs', 'attention_nmax12',
+                                  'attention_single_nodes', 'attention_heavy_dropout'])
 def test_fused_path_edge_shapes(gpu, case):
     """Fused-kernel boundaries against the oracle: a single node type (d_in = 1), the
     largest one-hot width the fused kernel takes (d_in = 32), Padding / NTN width 12 with
     12-node graphs (the third Â k-step full), dropout 0.9 (most elements dropped), and
-    self-pairs (g, g) plus repeated pairs (distinct pair keys, so distinct masks)."""
+    self-pairs (g, g) plus repeated pairs (distinct pair keys, so distinct masks); the
+    Attention-pooling kernel at capacity 12, on 1- to 4-node graphs and at dropout 0.9."""
     kw = dict(n_graphs=14, n_pairs=48, seed=17)
     if case == 'one_type':
         kw.update(n_types=1)
@@ -178,6 +185,12 @@ def test_fused_path_edge_shapes(gpu, case):
         kw.update(n_max=12, n_lo=9, n_hi=12)
     elif case == 'heavy_dropout':
         kw.update(flags_overrides=dict(dropout=0.9))
+    elif case == 'attention_nmax12':
+        kw.update(n_max=12, n_lo=9, n_hi=12, flags_overrides=STACKS['attention'])
+    elif case == 'attention_single_nodes':
+        kw.update(n_lo=1, n_hi=4, flags_overrides=STACKS['attention'])
+    elif case == 'attention_heavy_dropout':
+        kw.update(flags_overrides=dict(STACKS['attention'], dropout=0.9))
     prob = small_problem(**kw)
     if case == 'self_and_repeated_pairs':
         prob.pairs[:16, 1] = prob.pairs[:16, 0]

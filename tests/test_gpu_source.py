@@ -10,12 +10,13 @@ from _fixtures import AVERAGE_STACK, small_problem
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize('stack', ['default', 'average'])
+@pytest.mark.parametrize('stack', ['default', 'average', 'attention'])
 def test_fused_store_source_matches_records(gpu, stack):
     import torch
     from graphembedding_amd import _lib
     from graphembedding_amd.packer import GraphStore
-    ov = dict(AVERAGE_STACK) if stack == 'average' else {}
+    ov = {'default': {}, 'average': dict(AVERAGE_STACK),
+          'attention': dict(AVERAGE_STACK, layer_2='Attention:input_dim=16')}[stack]
     prob = small_problem(n_graphs=40, n_pairs=8, seed=31, n_lo=1, n_hi=10, n_max=10,
                          flags_overrides=ov)
     model, _ = prob.make_gpu_model(device=gpu)

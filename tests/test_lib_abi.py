@@ -58,7 +58,10 @@ def test_validate_paths_and_param_counts(L):
     assert path3 == 1 and n3 == avg.params.size           # tuning.py stack → fused (AVG)
     att = small_problem(flags_overrides=dict(AVERAGE_STACK, layer_2='Attention:input_dim=16'))
     n4, path4 = _lib.validate(_model(att))
-    assert path4 == 0 and n4 == att.params.size           # generic kernel
+    assert path4 == 1 and n4 == att.params.size           # Attention pooling → fused (ATT)
+    dot = small_problem(flags_overrides=dict(num_layers=5, layer_4='Dot'))
+    n5, path5 = _lib.validate(_model(dot))
+    assert path5 == 0 and n5 == dot.params.size           # generic kernel
     assert _lib.workspace_bytes(_model(prob), 490000) > 0
 
 
@@ -91,8 +94,8 @@ def test_store_source_checks(L):
     import torch
     fake = torch.zeros(4, dtype=torch.int32)   # host tensors: only the pointers are read
     dev = (fake, fake, fake)
-    att = small_problem(flags_overrides=dict(AVERAGE_STACK, layer_2='Attention:input_dim=16'))
-    m0 = _model(att)                                               # generic path 0
+    dot = small_problem(flags_overrides=dict(num_layers=5, layer_4='Dot'))
+    m0 = _model(dot)                                               # generic path 0
     assert _lib.validate(m0)[1] == 0
     with pytest.raises(_lib.SiameseHipError, match='SG_ERR_UNSUPPORTED'):
         _lib.pair_order_src(m0, _lib.pair_source(dev, 10), 4, fake, fake, stream=0)
