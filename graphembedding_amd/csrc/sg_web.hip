@@ -482,9 +482,18 @@ constexpr int SCS = 20, SCR = 16 * SCS;
 #ifndef SG_WEB_GS0_ROW
 #define SG_WEB_GS0_ROW 1
 #endif
+// Backward MFMAs on split-bf16 (round 4): gD1 = gS1·W1ᵀ as three v_mfma_f32_16x16x32_bf16
+// per feature half against W1's bf16 parts built once per block (the six leading products
+// of (h + m + l)(H + M + L), ≈ f32 accuracy; sg_fast's gD1), and the one-hot gW0 = Xᵀ·gS0 as
+// three v_mfma_f32_16x16x16_bf16 per (type tile, feature half) on the h, m and l parts of
+// gS0 (one-hot is exact in bf16) — 16-cycle / 8-cycle bf16 MFMAs that co-issue with VALU in
+// place of 32-cycle f32 ones that do not.  0: the f32 MFMAs (A/B)
+#ifndef SG_WEB_BF16_BWD
+#define SG_WEB_BF16_BWD 1
+#endif
 
 struct GcnLds {
-  int w0, b0, w1, w1t, b1, wd, tables, et, gx, z1, d1, scr, rp, col, val, total;
+  int w0, b0, w1, w1t, b1, wd, w1b, tables, et, gx, z1, d1, scr, rp, col, val, total;
 };
 
 __host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, int max_nnz, bool bwd, bool lcsr) {
@@ -497,6 +506,8 @@ __host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, int max_nnz, bool b
   L.b1 = o; o += WH2;
   L.wd = o; o += WH2;
   o = (o + 3) & ~3;
+  // backward: [cb][term][lane] uint4 bf16 B operands of gD1 (SG_WEB_BF16_BWD)
+  L.w1b = o; if (bwd && SG_WEB_BF16_BWD) o += 2 * 3 * 64 * 4;
   L.tables = o;
   L.et = o; o += n16;
   L.gx = o; if (bwd) o += n16;
@@ -596,6 +607,21 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
     sW1[x] = v;
     sW1T[(x % WH2) * WH1 + x / WH2] = v;
   }
+#if SG_WEB_BF16_BWD
+  // gD1's B operands: lane (i, g) of feature half cb holds the parts of
+  // W1[16cb + i][4g..4g+3]·ik1 as (H | H), (M | H), (L | M) (k-slots 8g..8g+7)
+  uint4 *sW1B = (uint4 *)(sm + L.w1b);
+  if (BWD)
+    for (int x = tid; x < 2 * 3 * 64; x += NT) {
+      const int cb = x / 192, term = (x / 64) % 3, ln = x & 63;
+      const float *wr = prm + A.oW1 + (16 * cb + (ln & 15)) * WH2 + 4 * (ln >> 4);
+      uint32_t h01, m01, l01, h23, m23, l23;
+      sgk::split3(wr[0] * A.ik1, wr[1] * A.ik1, h01, m01, l01);
+      sgk::split3(wr[2] * A.ik1, wr[3] * A.ik1, h23, m23, l23);
+      sW1B[x] = term == 0 ? uint4{h01, h23, h01, h23}
+                          : (term == 1 ? uint4{m01, m23, h01, h23} : uint4{l01, l23, m01, m23});
+    }
+#endif
   if (tid < WH1) sb0[tid] = prm[A.ob0 + tid];
   if (tid < WH2) {
     sb1[tid] = prm[A.ob1 + tid];
@@ -881,10 +907,26 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
         });
       // gD1·ik1 (rows n = 16t + 4g + r, column f = 16cb + i)
       f4 gd[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+#if SG_WEB_BF16_BWD
+      {   // A k-slots 8g..8g+7 = (h | m) or (h | l) of gS1[n][4g..4g+3]: hH + mH + hM + lH + hL + mM
+        uint32_t h01, m01, l01, h23, m23, l23;
+        sgk::split3(q4[0], q4[1], h01, m01, l01);
+        sgk::split3(q4[2], q4[3], h23, m23, l23);
+        const uint4 ahm = {h01, h23, m01, m23}, ahl = {h01, h23, l01, l23};
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const uint4 *wb = sW1B + cb * 192 + l;
+          gd[cb] = sgk::mfbf(ahm, wb[0], gd[cb]);
+          gd[cb] = sgk::mfbf(ahl, wb[64], gd[cb]);
+          gd[cb] = sgk::mfbf(ahm, wb[128], gd[cb]);
+        }
+      }
+#else
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
         for (int s = 0; s < 4; ++s) gd[cb] = mfma4(q4[s], sW1T[(4 * g + s) * WH1 + 16 * cb + i], gd[cb]);
+#endif
       // the tile's gS1 through the wave's scratch, read back as the B operand of gW1
       *(float4 *)(scr + i * SCS + 4 * g) = make_float4(q4[0], q4[1], q4[2], q4[3]);
       sg_wsync();
@@ -933,6 +975,18 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
       int et[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) et[s] = sEtk[16 * t + 4 * g + s];
+#if SG_WEB_BF16_BWD
+      // one-hot Xᵀ as a bf16 A operand: row i ↔ type 16tb + i, k-slot 4g + s ↔ node
+      // 16t + 4g + s (v_mfma_f32_16x16x16_bf16: 4 k-slots per lane)
+      uint2 oh[NTB];
+#pragma unroll
+      for (int tb = 0; tb < NTB; ++tb) {
+        uint32_t o[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) o[s] = et[s] == 16 * tb + i ? 0x3F80u : 0u;   // bf16 1.0
+        oh[tb] = uint2{o[0] | (o[1] << 16), o[2] | (o[3] << 16)};
+      }
+#endif
       // per feature half c: the tile through the scratch, read back as the B operand
       // (k-slot g ↔ node 16t + 4g + s, column i ↔ feature 16c + i)
 #pragma unroll
@@ -945,6 +999,17 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) bq[s] = scr[(4 * g + s) * SCS + i];
         sg_wsync();
+#if SG_WEB_BF16_BWD
+        uint32_t h01, m01, l01, h23, m23, l23;
+        sgk::split3(bq[0], bq[1], h01, m01, l01);
+        sgk::split3(bq[2], bq[3], h23, m23, l23);
+#pragma unroll
+        for (int tb = 0; tb < NTB; ++tb) {
+          aW0[tb][c] = sgk::mfbf16(oh[tb], uint2{l01, l23}, aW0[tb][c]);
+          aW0[tb][c] = sgk::mfbf16(oh[tb], uint2{m01, m23}, aW0[tb][c]);
+          aW0[tb][c] = sgk::mfbf16(oh[tb], uint2{h01, h23}, aW0[tb][c]);
+        }
+#else
 #pragma unroll
         for (int tb = 0; tb < NTB; ++tb)
 #pragma unroll
@@ -952,6 +1017,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
             const float a = et[s] == 16 * tb + i ? 1.f : 0.f;
             aW0[tb][c] = mfma4(a, bq[s], aW0[tb][c]);
           }
+#endif
       }
 #else
       float bq[4][2];
