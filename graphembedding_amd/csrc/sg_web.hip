@@ -1361,6 +1361,133 @@ __global__ void __launch_bounds__(256) web_t_kernel_b3(const float *__restrict__
     }
 }
 
+// ---- T with TKG feature maps k per block (round 4, SG_WEB_TKG, default): web_t_kernel_b3
+// re-fetched a pair block's x2 rows for each of its K x (a-tiles) tiles (18.45 GB per
+// 524,288-pair chunk against ≈0.5 GB of x rows, rocprof FETCH_SIZE).  Here one 8-wave block
+// stages the x2 chunk once for TKG = 4 feature maps k (the B operands of the four W[k]
+// planes beside it: 150 KB of LDS, one block per CU), so x2 is fetched ceil(K / 4) times per
+// a-tile instead of K times.  Wave w: k = 4 kg + 2 (w >> 2) + {0, 1}, 64x64 sub-tile
+// ((w >> 1) & 1, w & 1).  Per (k, tile) the MFMA order is web_t_kernel_b3's, so MP is bitwise
+// the same.
+#ifndef SG_WEB_TKG
+#define SG_WEB_TKG 1
+#endif
+constexpr int TKG = 4;
+__global__ void __launch_bounds__(512) web_t_kernel_kg(const float *__restrict__ X2,
+                                                       const float *__restrict__ Wg,
+                                                       const int2 *__restrict__ ext128, int64_t n,
+                                                       int Dp, int K, float *__restrict__ Tout,
+                                                       const float *__restrict__ X1) {
+  __shared__ __attribute__((aligned(16))) uint16_t sA[3 * B3PART], sB[TKG][3 * B3PART];
+  __shared__ float mred[TKG][2][TB];
+  const int pbk = (int)blockIdx.x, at = (int)blockIdx.y, kg = (int)blockIdx.z;
+  if ((int64_t)pbk * TB >= n) return;
+  const int64_t p0 = (int64_t)pbk * TB;
+  const int a0 = at * TB;
+  const int2 e = ext128[pbk];
+  if (a0 >= e.x) return;
+  const int nb = (e.y + B3K - 1) / B3K * B3K;   // x2 is zero past n2 (Dp is a multiple of 128)
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, i = l & 15, g = l >> 4;
+  const int wk = w >> 2, wm = (w >> 1) & 1, wn = w & 1;
+  const int k0 = kg * TKG;
+  const int nk = K - k0 < TKG ? K - k0 : TKG;   // feature maps of this block
+  const float *pa = X2 + p0 * Dp;
+  float4 ra[2], rb[TKG][2];
+  auto load = [&](int b0) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = tid + 512 * u, r = q >> 3, c = (q & 7) * 4;
+      ra[u] = *(const float4 *)(pa + (size_t)r * Dp + b0 + c);
+#pragma unroll
+      for (int kk = 0; kk < TKG; ++kk)
+        if (kk < nk)
+          rb[kk][u] = *(const float4 *)(Wg + ((size_t)(k0 + kk) * Dp + a0 + r) * Dp + b0 + c);
+    }
+  };
+  f4 acc[2][4][4];
+#pragma unroll
+  for (int kx = 0; kx < 2; ++kx)
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) acc[kx][mi][ni] = f4{0.f, 0.f, 0.f, 0.f};
+  if (nb > 0) load(0);
+  for (int b0 = 0; b0 < nb; b0 += B3K) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = tid + 512 * u, r = q >> 3, c = (q & 7) * 4;
+      b3_split_store(sA, r, c, ra[u]);
+#pragma unroll
+      for (int kk = 0; kk < TKG; ++kk)
+        if (kk < nk) b3_split_store(sB[kk], r, c, rb[kk][u]);
+    }
+    __syncthreads();
+    if (b0 + B3K < nb) load(b0 + B3K);
+    // A fragments of two row groups mi at a time (the registers of all four, beside the
+    // accumulators of two k and the next chunk's loads, would spill)
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh) {
+    uint4 ah[2], am[2], al[2];
+#pragma unroll
+    for (int m2 = 0; m2 < 2; ++m2) {
+      const int oa = (wm * 64 + (2 * mh + m2) * 16 + i) * B3S + 8 * g;
+      ah[m2] = *(const uint4 *)(sA + oa);
+      am[m2] = *(const uint4 *)(sA + B3PART + oa);
+      al[m2] = *(const uint4 *)(sA + 2 * B3PART + oa);
+    }
+#pragma unroll
+    for (int kx = 0; kx < 2; ++kx) {
+      const int kk = 2 * wk + kx;
+      if (kk >= nk) continue;
+      const uint16_t *sb = sB[kk];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int ob = (wn * 64 + ni * 16 + i) * B3S + 8 * g;
+        const uint4 bh = *(const uint4 *)(sb + ob), bm = *(const uint4 *)(sb + B3PART + ob),
+                    bl = *(const uint4 *)(sb + 2 * B3PART + ob);
+#pragma unroll
+        for (int m2 = 0; m2 < 2; ++m2) {
+          const int mi = 2 * mh + m2;
+          f4 c = acc[kx][mi][ni];
+          c = sgk::mfbf(al[m2], bh, c);
+          c = sgk::mfbf(ah[m2], bl, c);
+          c = sgk::mfbf(am[m2], bm, c);
+          c = sgk::mfbf(am[m2], bh, c);
+          c = sgk::mfbf(ah[m2], bm, c);
+          c = sgk::mfbf(ah[m2], bh, c);
+          acc[kx][mi][ni] = c;
+        }
+      }
+    }
+    }
+    __syncthreads();
+  }
+  // the tile's share of the bilinear term per k, as web_t_kernel_b3<true>
+#pragma unroll
+  for (int kx = 0; kx < 2; ++kx) {
+    const int kk = 2 * wk + kx;
+    if (kk >= nk) continue;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int pl = wm * 64 + mi * 16 + 4 * g + r;
+        const float *x1 = X1 + (p0 + pl) * Dp + a0 + wn * 64 + i;
+        float part = 0.f;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) part = fmaf(x1[ni * 16], acc[kx][mi][ni][r], part);
+        part = sgk::row_sum16(part);
+        if (i == 0) mred[kk][wn][pl] = part;
+      }
+  }
+  __syncthreads();
+  {
+    const int kk = tid >> 7, pr = tid & 127;
+    if (kk < nk && p0 + pr < n)
+      Tout[((p0 + pr) * WKP + k0 + kk) * 4 + at] = mred[kk][0][pr] + mred[kk][1][pr];
+  }
+}
+
 // ---- gX2[p][b] += Σ_{k,a} gm[p][k] x1[p][a] W[a][b][k]  (grid: p-blocks × b-tiles) ----
 __global__ void __launch_bounds__(256) web_gx2_kernel(const float *__restrict__ X1,
                                                       const float *__restrict__ GM,
@@ -2350,7 +2477,13 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     const int64_t c0 = c * chunk, n = n_pairs - c0 < chunk ? n_pairs - c0 : chunk;
     const int64_t nblk = (n + TB - 1) / TB;
     float *X = S.X, *GX = S.GX, *T = S.T, *GM = S.GM;
-    if (SG_WEB_T_BF3)
+    // SG_WEB_TKG=0: web_t_kernel_b3, one k per block (read per call: a test compares the two)
+    const char *tkg_e = getenv("SG_WEB_TKG");
+    const bool tkg = SG_WEB_TKG && !(tkg_e && tkg_e[0] == '0');
+    if (SG_WEB_T_BF3 && tkg)
+      hipLaunchKernelGGL(web_t_kernel_kg, dim3((unsigned)nblk, Dp / TB, (K + TKG - 1) / TKG),
+                         dim3(512), 0, gs, X + ws.Cp * Dp, Wg, S.EXT128, n, Dp, K, T, X);
+    else if (SG_WEB_T_BF3)
       hipLaunchKernelGGL(web_t_kernel_b3<true>, web_pb_grid(nblk, Dp / TB, K), dim3(256),
                          web_lds_pad("SG_WEB_TPAD", (const void *)web_t_kernel_b3<true>), gs,
                          X + ws.Cp * Dp, Wg, S.EXT128, n, Dp, K, T, X);

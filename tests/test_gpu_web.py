@@ -142,6 +142,29 @@ def test_web_pipeline_is_bitwise_the_serial_sequence(gpu, monkeypatch):
         assert torch.equal(a, b)
 
 
+def test_web_t_kernel_k_groups_are_bitwise(gpu, monkeypatch):
+    """The T GEMM with four feature maps per block (web_t_kernel_kg: the x2 chunk staged once
+    for four W[k] planes) keeps web_t_kernel_b3's MFMA order per (k, tile): scores, gradient
+    and loss bitwise those of one k per block, K = 10 (groups 4, 4, 2) and K = 16."""
+    import torch
+    for K in (10, 16):
+        ov = dict(layer_3='Padding:max_in_dims=256,padding_value=0',
+                  layer_4='NTN:input_dim=256,feature_map_dim={},inneract=relu,dropout=True,'
+                          'bias=True'.format(K))
+        prob = small_problem(n_graphs=20, n_pairs=600, seed=23, n_lo=20, n_hi=250, n_max=256,
+                             flags_overrides=ov, p_extra=0.03)
+        model, chunked = prob.make_gpu_web_model(device=gpu, chunk=251)
+        out = {}
+        for mode in ('1', '0'):
+            monkeypatch.setenv('SG_WEB_TKG', mode)
+            s = model.pred_sim_without_act(chunked, seed=3).clone()
+            model.fwd_bwd(chunked, seed=3)
+            torch.cuda.synchronize()
+            out[mode] = (s, model.grad.clone(), model.loss_buf.clone())
+        for a, b in zip(out['1'], out['0']):
+            assert torch.equal(a, b), K
+
+
 def test_web_xcd_units_match_flat_units(gpu, monkeypatch):
     """The XCD-partitioned unit order (instances of graph g on the blocks of partition
     g % 8) changes only which workgroup runs an instance: scores and loss are bitwise
