@@ -368,8 +368,11 @@ def main():
         if web:
             workload = ('Web-sized all-pairs ({} synthetic graphs, N ~ U{{64..512}}, {:,} ordered '
                         'pairs), Padding/NTN 512'.format(len(gs.graphs), total_pairs))
+            ws_gb = _lib.web_workspace_bytes(model.sg, shard.chunk) / 1e9
             inputs = ('CSR graph store + size-ordered pair ids resident in HBM, {} pairs per '
-                      'internal chunk'.format(shard.chunk))
+                      'internal chunk; workspace {:.1f} GB (two pipeline slots of NTN inputs, '
+                      'keep bits and D2 rows at node capacity {})'.format(
+                          shard.chunk, ws_gb, gs.n_max))
             records = 'CSR store (no pair records), {:.0f} B/pair of graph input'.format(bytes_pair)
         else:
             workload = ('AIDS10knef all-pairs (10,018 graphs, N <= 30, {:,} ordered '

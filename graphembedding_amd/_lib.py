@@ -153,6 +153,8 @@ def lib():
     pc = ctypes.POINTER(SgCsrStore)
     L.sg_web_workspace_bytes.argtypes = [pm, c_i64]
     L.sg_web_workspace_bytes.restype = c_i64
+    L.sg_web_workspace_bytes_ex.argtypes = [pm, c_i64, c_i64]
+    L.sg_web_workspace_bytes_ex.restype = c_i64
     L.sg_web_forward.argtypes = [pm, pc, vp, c_i64, c_i64, vp, c_u64, vp, vp, c_i64, vp]
     L.sg_web_forward.restype = c_i32
     L.sg_web_fwd_bwd.argtypes = [pm, pc, vp, vp, c_i64, c_i64, c_i64, vp, c_u64, vp, c_i32, vp,
@@ -179,6 +181,7 @@ EXPORTED_SYMBOLS = ('sg_version', 'sg_record_bytes', 'sg_record_bytes_ex', 'sg_m
                     'sg_forward_ex', 'sg_fwd_bwd_ex', 'sg_pair_order',
                     'sg_pair_order_workspace_bytes', 'sg_sampler_random', 'sg_sampler_density',
                     'sg_adam_workspace_bytes', 'sg_adam_tf_ex', 'sg_web_workspace_bytes',
+                    'sg_web_workspace_bytes_ex',
                     'sg_web_forward', 'sg_web_fwd_bwd', 'sg_fwd_bwd_dseed', 'sg_seed_advance',
                     'sg_feed_step', 'sg_pair_order_src', 'sg_forward_src', 'sg_fwd_bwd_src',
                     'sg_pair_order_cls', 'sg_forward_cls', 'sg_fwd_bwd_cls')
@@ -459,8 +462,13 @@ def csr_struct(n_graphs, n_max, node_off, types, row_ptr, col, val, max_nnz=0) -
     return s
 
 
-def web_workspace_bytes(m: SgModel, chunk: int) -> int:
-    b = int(lib().sg_web_workspace_bytes(ctypes.byref(m), int(chunk)))
+def web_workspace_bytes(m: SgModel, chunk: int, n_pairs: int = -1) -> int:
+    """Workspace of sg_web_* calls in chunks of `chunk`; n_pairs >= 0: calls of at most
+    n_pairs pairs (one pipeline slot when n_pairs <= chunk, sg_web_workspace_bytes_ex)."""
+    if n_pairs >= 0:
+        b = int(lib().sg_web_workspace_bytes_ex(ctypes.byref(m), int(chunk), int(n_pairs)))
+    else:
+        b = int(lib().sg_web_workspace_bytes(ctypes.byref(m), int(chunk)))
     if b < 0:
         raise SiameseHipError('sg_web_workspace_bytes: model is not on the graph-store path')
     return b

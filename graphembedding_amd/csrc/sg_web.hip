@@ -149,7 +149,9 @@ struct WebWs {
   int64_t MASK;   // uint16 [2 Cp][Dp][4]: the forward's dropout keep bits per (instance, node, g)
   int64_t D2;     // [2 Cp][Dp][16]: the forward's D2 = dropout(H2) per (instance, node)
   int64_t SLOT;                                      // floats per slot
-  int64_t Wg, Wh, GWS, GVS, GSLAB, HSLABo, total;    // per-call buffers
+  int64_t S0;                                        // slot 0 (slot 1 = S0 + SLOT, last)
+  int64_t Wg, Wh, GWS, GVS, GSLAB, HSLABo;           // per-call buffers (first)
+  int64_t total, total1;   // with both slots; with slot 0 only (calls of one chunk)
   int gcn_blocks, head_blocks;
 };
 
@@ -182,6 +184,18 @@ WebWs web_ws(const WebPlan &W, int64_t chunk) {
   const int64_t Dp = W.Dp, K = W.K;
   int64_t o = 0;
   auto take = [&](int64_t n) { const int64_t r = o; o += (n + 63) & ~(int64_t)63; return r; };
+  // per-call buffers first, then the pipeline slots, slot 1 last: a call of one chunk
+  // (n_pairs <= chunk) never pipelines and needs total1 floats only
+  w.Wg = take(K * Dp * Dp);
+  w.Wh = take(K * Dp * Dp);
+  w.GWS = take((int64_t)WSPLIT * K * Dp * Dp);
+  w.GVS = take((int64_t)WSPLIT * WKP * 2 * Dp);
+  w.gcn_blocks = gcn_blocks_for();
+  w.head_blocks = head_blocks_for();
+  w.GSLAB = take((int64_t)w.gcn_blocks * W.n_gcn);
+  w.HSLABo = take((int64_t)w.head_blocks * 4 * HSLAB);
+  w.S0 = o;
+  o = 0;   // slot-relative offsets
   w.X = take(2 * w.Cp * Dp);        // X1 | X2
   w.GX = take(2 * w.Cp * Dp);       // gX1 | gX2
   // T: the a-tile shares MP[p][k][4] of web_t_kernel_b3<true>, or all of T (f32 path)
@@ -197,16 +211,8 @@ WebWs web_ws(const WebPlan &W, int64_t chunk) {
   w.MASK = take(4 * w.Cp * Dp);     // 2 Cp x Dp x 4 uint16
   w.D2 = SG_WEB_D2 ? take(32 * w.Cp * Dp) : 0;   // 2 Cp x Dp x 16
   w.SLOT = o;
-  o += w.SLOT;                      // slot 1
-  w.Wg = take(K * Dp * Dp);
-  w.Wh = take(K * Dp * Dp);
-  w.GWS = take((int64_t)WSPLIT * K * Dp * Dp);
-  w.GVS = take((int64_t)WSPLIT * WKP * 2 * Dp);
-  w.gcn_blocks = gcn_blocks_for();
-  w.head_blocks = head_blocks_for();
-  w.GSLAB = take((int64_t)w.gcn_blocks * W.n_gcn);
-  w.HSLABo = take((int64_t)w.head_blocks * 4 * HSLAB);
-  w.total = o;
+  w.total1 = w.S0 + w.SLOT;
+  w.total = w.S0 + 2 * w.SLOT;
   return w;
 }
 
@@ -2210,10 +2216,13 @@ int sg_web_plan_params(const sg_model_t *m, int64_t *n_params) {
   return rc;
 }
 
-int64_t sg_web_ws_bytes(const sg_model_t *m, int64_t chunk) {
+int64_t sg_web_ws_bytes(const sg_model_t *m, int64_t chunk, int64_t n_pairs) {
   WebPlan W;
   if (web_plan(m, &W) != SG_OK) return -1;
-  return web_ws(W, chunk).total * 4 + 256;
+  const WebWs ws = web_ws(W, chunk);
+  // calls of at most one chunk never pipeline (sg_web_run): slot 0 only
+  const bool one = n_pairs >= 0 && n_pairs <= (chunk > 0 ? chunk : 1);
+  return (one ? ws.total1 : ws.total) * 4 + 256;
 }
 
 // A/B: dynamic LDS padding of a GEMM launch (bytes, from the environment), which lowers the
@@ -2423,7 +2432,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     int32_t *isort, *icnt, *icls;
   };
   auto slot = [&](int64_t c) {
-    float *sb = base + (pipe ? (c & 1) * ws.SLOT : 0);
+    float *sb = base + ws.S0 + (pipe ? (c & 1) * ws.SLOT : 0);
     Slot S;
     S.X = sb + ws.X; S.GX = sb + ws.GX; S.T = sb + ws.T; S.GM = sb + ws.GM;
     S.EXT = (int2 *)(sb + ws.EXT); S.EXT16 = (int2 *)(sb + ws.EXT16);

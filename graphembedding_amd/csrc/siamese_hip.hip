@@ -43,7 +43,7 @@ int sg_fast32_supported(const sg_model_t *m, const SgGenPlan &P);
 // graph-store path for Web-sized graphs (sg_web.hip)
 int sg_web_plan_params(const sg_model_t *m, int64_t *n_params);
 int sg_web_lds_ok(const sg_model_t *m);
-int64_t sg_web_ws_bytes(const sg_model_t *m, int64_t chunk);
+int64_t sg_web_ws_bytes(const sg_model_t *m, int64_t chunk, int64_t n_pairs);
 int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *pairs,
                const float *labels, int64_t n_pairs, int64_t pair_offset, int64_t batch_total,
                const float *params, uint64_t seed, const float *y_stats, int add_label,
@@ -499,7 +499,7 @@ int64_t ntn_offset_floats(const PathChoice &c, int64_t n_pairs) {
 // ===========================================================================
 extern "C" {
 
-int32_t sg_version(void) { return 10700; }   /* 1.7.0: class-exclusive schedule (sg_*_cls) */
+int32_t sg_version(void) { return 10800; }   /* 1.8.0: sg_web_workspace_bytes_ex; fused Attention pooling */
 
 int64_t sg_record_bytes(int32_t n_max) { return sg_record_bytes_ex(n_max, SG_DTYPE_F32); }
 
@@ -884,7 +884,12 @@ int32_t sg_adam_tf_ex(float *params, float *m, float *v, const float *grad, int6
 
 int64_t sg_web_workspace_bytes(const sg_model_t *model, int64_t chunk) {
   if (!model || chunk < 0) return -1;
-  return sg_web_ws_bytes(model, chunk);
+  return sg_web_ws_bytes(model, chunk, -1);   // any n_pairs: both pipeline slots
+}
+
+int64_t sg_web_workspace_bytes_ex(const sg_model_t *model, int64_t chunk, int64_t n_pairs) {
+  if (!model || chunk < 0 || n_pairs < 0) return -1;
+  return sg_web_ws_bytes(model, chunk, n_pairs);
 }
 
 int32_t sg_web_forward(const sg_model_t *model, const sg_csr_store_t *store,

@@ -181,7 +181,7 @@ class SiameseGCNTNMSE(object):
         if batch.csr is not None:
             _lib.web_forward(self.sg, batch.csr.to_device(self.device), batch.pairs, batch.n_pairs,
                              batch.pair_offset, self.params, self._seed(seed), s,
-                             self.web_workspace(batch.chunk), batch.chunk)
+                             self.web_workspace(batch.chunk, batch.n_pairs), batch.chunk)
             return s
         if batch.src is not None:
             _lib.forward_src(self.sg, batch.src, batch.n_pairs, batch.pair_offset, self.params,
@@ -275,14 +275,20 @@ class SiameseGCNTNMSE(object):
         b.chunk = int(chunk or min(max(n, 1), 32768))
         return b
 
-    def web_workspace(self, chunk):
+    def web_workspace(self, chunk, n_pairs=-1):
+        """Graph-store workspace for calls of up to n_pairs pairs in chunks of `chunk`
+        (n_pairs <= chunk: one pipeline slot, about half the bytes; -1: any n_pairs).  A
+        cached workspace is reused when it is at least as large as the call needs."""
         torch = self.torch
-        key = ('web', int(chunk))
-        if getattr(self, '_web_ws_key', None) != key:
-            nbytes = _lib.web_workspace_bytes(self.sg, int(chunk))
-            self._web_ws = None
-            self._web_ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device=self.device)
-            self._web_ws_key = key
+        one = 0 <= int(n_pairs) <= int(chunk)
+        key = ('web', int(chunk), one)
+        have = getattr(self, '_web_ws_key', None)
+        if have is not None and have[:2] == key[:2] and (not have[2] or one):
+            return self._web_ws
+        nbytes = _lib.web_workspace_bytes(self.sg, int(chunk), 0 if one else -1)
+        self._web_ws = None
+        self._web_ws = torch.empty(nbytes // 4 + 64, dtype=torch.float32, device=self.device)
+        self._web_ws_key = key
         return self._web_ws
 
     def batch_from_records(self, recs, n_pairs, labels, pair_offset=0, batch_total=None,
@@ -358,8 +364,8 @@ class SiameseGCNTNMSE(object):
             _lib.web_fwd_bwd(self.sg, batch.csr.to_device(self.device), batch.pairs, batch.labels,
                              batch.n_pairs, batch.pair_offset, batch.batch_total, self.params,
                              self._seed(seed), batch.y_stats, 1 if add_label_term else 0, s_out,
-                             self.grad, self.loss_buf, self.web_workspace(batch.chunk),
-                             batch.chunk)
+                             self.grad, self.loss_buf,
+                             self.web_workspace(batch.chunk, batch.n_pairs), batch.chunk)
             return
         if batch.src is not None:
             _lib.fwd_bwd_src(self.sg, batch.src, batch.n_pairs, batch.pair_offset,

@@ -352,6 +352,14 @@ typedef struct sg_csr_store {
  * to `chunk` pairs (any n_pairs is processed chunk by chunk). */
 int64_t sg_web_workspace_bytes(const sg_model_t *model, int64_t chunk);
 
+/* Workspace bytes for sg_web_forward / sg_web_fwd_bwd calls of at most n_pairs pairs in
+ * chunks of `chunk` (library 1.8).  A call of several chunks pipelines them over two
+ * workspace slots (the NTN inputs, dropout keep bits and D2 rows of one chunk each, which
+ * grow with chunk x node capacity); when n_pairs <= chunk there is one chunk and one slot,
+ * about half of sg_web_workspace_bytes.  A workspace sized for n_pairs serves calls of up
+ * to n_pairs pairs. */
+int64_t sg_web_workspace_bytes_ex(const sg_model_t *model, int64_t chunk, int64_t n_pairs);
+
 /* Pre-activation scores of the pairs pair_idx [n_pairs][2] (store graph ids);
  * replaces sess.run([pred_sim_without_act()]) like sg_forward. */
 int32_t sg_web_forward(const sg_model_t *model, const sg_csr_store_t *store,

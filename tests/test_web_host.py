@@ -93,3 +93,17 @@ def test_web_allpairs_shards_partition_the_list():
     assert np.array_equal(lab, labels[cat[:, 0], cat[:, 1]])
     assert all(np.allclose(p.y_stats.numpy(), full.y_stats.numpy()) for p in parts)
     assert [p.start for p in parts] == [0, parts[0].end, parts[1].end]
+
+
+def test_workspace_one_slot_for_single_chunk_calls():
+    """sg_web_workspace_bytes_ex: a call of at most one chunk never pipelines, so it needs
+    one of the two per-chunk slots; several chunks need both, as
+    sg_web_workspace_bytes reports."""
+    prob = small_problem(n_graphs=6, n_pairs=6, n_lo=20, n_hi=60, n_max=64)
+    m = _model(prob, 64)
+    two = _lib.web_workspace_bytes(m, 4096)
+    assert _lib.web_workspace_bytes(m, 4096, 4097) == two
+    one = _lib.web_workspace_bytes(m, 4096, 4096)
+    assert one == _lib.web_workspace_bytes(m, 4096, 0) and one < two
+    # the slots dominate: the second one is most of the difference from the per-call part
+    assert two - one > 0.4 * two
