@@ -70,6 +70,21 @@ def parse():
     return p.parse_args()
 
 
+def fused_kernel_source_hash() -> str:
+    """sha1 over the headline fused kernel's sources (csrc/sg_fast.hip and the headers it
+    includes): profiles/traffic.json records it, and the bench line reports that file's
+    PMC traffic only while the tree still hashes the same."""
+    import hashlib
+    h = hashlib.sha1()
+    csrc = os.path.join(ROOT, 'graphembedding_amd', 'csrc')
+    for f in ('sg_fast.hip', 'sg_mfma.h', 'sg_plan.h', 'sg_common.h'):
+        with open(os.path.join(csrc, f), 'rb') as fh:
+            h.update(fh.read())
+    with open(os.path.join(ROOT, 'include', 'siamese_hip.h'), 'rb') as fh:
+        h.update(fh.read())
+    return h.hexdigest()
+
+
 def cpu_baseline(gs, labels, flags, n_sample, D=None):
     """Time the oracle's C restatement (oracle/siamese_cpu.c, OpenMP) on a
     bounded sample of the same all-pairs stream, on this host's cores (all of
@@ -345,11 +360,16 @@ def main():
                 t = json.load(f)
             # HBM bytes per launch: PMC counters cannot be read from inside this process,
             # so they come from the committed rocprofv3 --pmc passes of this same command
-            # on this tree (scripts/gpu_round3.sh + scripts/make_profile_summary.py)
-            traffic = t.get('traffic_bytes_per_launch') * shard.n / 490000.0
-            traffic_src = 'profiles/{}/traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE ' \
-                          'passes of bench.py --gpus 1; FETCH_SIZE x2 gfx950 correction)'.format(
-                              t.get('tree', '?'))
+            # on this tree (scripts/gpu_round3.sh + scripts/make_profile_summary.py), and
+            # only while the fused kernel's sources are the ones those passes measured
+            if t.get('sources_sha1') == fused_kernel_source_hash():
+                traffic = t.get('traffic_bytes_per_launch') * shard.n / 490000.0
+                traffic_src = ('profiles/{}/traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE '
+                               'passes of bench.py --gpus 1 on these kernel sources; FETCH_SIZE x2 '
+                               'gfx950 correction)'.format(t.get('tree', '?')))
+            else:
+                traffic_src = ('none: profiles/traffic.json ({}) was measured on other sg_fast '
+                               'sources'.format(t.get('tree', '?')))
         cpu = None
         if world == 1 and args.cpu_sample >= 0:
             try:

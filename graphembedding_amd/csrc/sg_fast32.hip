@@ -397,492 +397,514 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
     int N1 = __builtin_amdgcn_readfirstlane(ty[2 * NC + 1]);
     N0 = N0 < 0 ? 0 : (N0 > D ? D : N0);
     N1 = N1 < 0 ? 0 : (N1 > D ? D : N1);
-    const int KB0 = (N0 + 3) >> 2, KB1 = (N1 + 3) >> 2;   // k-blocks of 4 nodes
-    const int T0 = N0 > 16 ? 2 : 1, T1 = N1 > 16 ? 2 : 1;
-    const int KBm = KB0 > KB1 ? KB0 : KB1;
-    const uint32_t pk = sg_pair_key(A.key, (uint32_t)(A.pair_offset + p));
-    const float label = sRec[L::TAIL + 2 * NC + 2];
+    // The pair body per tile-count class (T0, T1) = (N0 > 16, N1 > 16) + 1: every tile loop and
+    // the first tile's k-blocks are straight-line code of the exact length, only the last
+    // tile's k-blocks keep a runtime test (KB <= 4 for one tile, KB >= 5 for two)
+    auto body = [&](auto T0c, auto T1c) __attribute__((always_inline)) {
+      const int KB0 = (N0 + 3) >> 2, KB1 = (N1 + 3) >> 2;   // k-blocks of 4 nodes
+      constexpr int T0 = decltype(T0c)::value, T1 = decltype(T1c)::value;   // tiles per side
+      constexpr int TM = T0 > T1 ? T0 : T1;
+      const int KBm = KB0 > KB1 ? KB0 : KB1;
+      // k-block b of a side with T tiles and KB k-blocks holds nodes: T = 1 has KB <= 4, T = 2
+      // has KB >= 5, so only the blocks of the last tile need the runtime test
+      auto kb_live = [&](int b, int T, int KB) __attribute__((always_inline)) -> bool {
+        return b < 4 * T && (b < 4 * (T - 1) || b < KB);
+      };
+      const uint32_t pk = sg_pair_key(A.key, (uint32_t)(A.pair_offset + p));
+      const float label = sRec[L::TAIL + 2 * NC + 2];
 
-    // ---- layer-0 (node) and NTN-input dropout masks: one hash per lane ----
-    // lanes 0..31: layer 0, node e = l; lanes 32..63: layer 4, element e = l - 32
-    uint32_t km0[2], km4[2];   // bit n ↔ node / element n of side s (0 when n >= N_s)
-    {
-      const int e = l & 31;
-      const bool hi = l >= 32;
-      const uint32_t h = sg_hash(pk, hi ? 4u : 0u, (uint32_t)e);
-      // both thresholds as scalar values first: a select between two kernel-argument
-      // fields compiled to a per-lane load from the argument block inside the pair loop
-      // (global_load + s_waitcnt vmcnt(0), which also waited for the next record's prefetch)
-      const uint32_t thr = hi ? thr4s : thr0s;
-      const uint64_t b0 = __ballot((e < N0) & ((h & 0xFFFFu) < thr));
-      const uint64_t b1 = __ballot((e < N1) & ((h >> 16) < thr));
-      km0[0] = (uint32_t)b0;
-      km4[0] = (uint32_t)(b0 >> 32);
-      km0[1] = (uint32_t)b1;
-      km4[1] = (uint32_t)(b1 >> 32);
-    }
+      // ---- layer-0 (node) and NTN-input dropout masks: one hash per lane ----
+      // lanes 0..31: layer 0, node e = l; lanes 32..63: layer 4, element e = l - 32
+      uint32_t km0[2], km4[2];   // bit n ↔ node / element n of side s (0 when n >= N_s)
+      {
+        const int e = l & 31;
+        const bool hi = l >= 32;
+        const uint32_t h = sg_hash(pk, hi ? 4u : 0u, (uint32_t)e);
+        // both thresholds as scalar values first: a select between two kernel-argument
+        // fields compiled to a per-lane load from the argument block inside the pair loop
+        // (global_load + s_waitcnt vmcnt(0), which also waited for the next record's prefetch)
+        const uint32_t thr = hi ? thr4s : thr0s;
+        const uint64_t b0 = __ballot((e < N0) & ((h & 0xFFFFu) < thr));
+        const uint64_t b1 = __ballot((e < N1) & ((h >> 16) < thr));
+        km0[0] = (uint32_t)b0;
+        km4[0] = (uint32_t)(b0 >> 32);
+        km0[1] = (uint32_t)b1;
+        km4[1] = (uint32_t)(b1 >> 32);
+      }
 
-    // Â A-fragments of side s: Â[node(to, j)][4b + g] for the side's tiles / k-blocks,
-    // re-read from the record image (intact for the whole pair) in each phase
-    auto load_af = [&](int s, int T, int KB, float (&af)[2][8]) __attribute__((always_inline)) {
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const int ab = abase0 + s * NC * RS + 4 * b;
-        // unconditional: entries past N are zero (record contract), and reads without a
-        // per-k-block branch issue together (one LDS round trip instead of one per block)
-#if SG32_AF_ALL
-        af[0][b] = W[ab];
-        af[1][b] = W[ab + 16 * RS];
-#else
-        af[0][b] = b < KB ? W[ab] : 0.f;
-        af[1][b] = (b < KB && T > 1) ? W[ab + 16 * RS] : 0.f;
-#endif
-      }
-    };
+      // Â A-fragments of side s: Â[node(to, j)][4b + g] for the side's tiles / k-blocks,
+      // re-read from the record image (intact for the whole pair) in each phase
+      auto load_af = [&](int s, int T, int KB, float (&af)[2][8]) __attribute__((always_inline)) {
+  #pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const int ab = abase0 + s * NC * RS + 4 * b;
+          // unconditional: entries past N are zero (record contract), and reads without a
+          // per-k-block branch issue together (one LDS round trip instead of one per block)
+  #if SG32_AF_ALL
+          af[0][b] = b < 4 * T ? W[ab] : 0.f;
+          af[1][b] = T > 1 ? W[ab + 16 * RS] : 0.f;
+  #else
+          af[0][b] = b < KB ? W[ab] : 0.f;
+          af[1][b] = (b < KB && T > 1) ? W[ab + 16 * RS] : 0.f;
+  #endif
+        }
+      };
 
-    // ================= forward: ik1 · P1 = Â Z0 + ik1 b0 =================
-    uint32_t tyA[2][2];     // [s][tile]: types of node rows 4g+r, 6 bits; 63 = dropped/absent
-    f4 d1[2][2][2];         // [s][to][f]: P1, then D1 in place
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int KB = s ? KB1 : KB0, T = s ? T1 : T0;
-      const uint32_t kms = km0[s];
-      uint32_t tp[2] = {0u, 0u};
-#pragma unroll
-      for (int to = 0; to < 2; ++to) {
-        d1[s][to][0] = f4{b0v0, b0v0, b0v0, b0v0};
-        d1[s][to][1] = f4{b0v1, b0v1, b0v1, b0v1};
-      }
-#if SG32_HOIST_P1
-      // types, W0 rows and Â fragments of all eight k-blocks first (unconditional reads,
-      // two dependent LDS round trips per side instead of two per k-block): nodes past N
-      // are masked (k0 = 0 -> the zero row d_in), Â is zero there
-      uint32_t t8[8];
-#pragma unroll
-      for (int b = 0; b < 8; ++b) t8[b] = (uint32_t)ty[s * NC + 4 * b + g];
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const uint32_t t_ = min(t8[b], (uint32_t)(d_in - 1));
-        const uint32_t k0 = (kms >> (4 * b + g)) & 1u;
-        t8[b] = k0 ? t_ : 63u;   // 63: dropped / absent (the W0 row read is d_in's zero row)
-        tp[b >> 2] |= t8[b] << (6 * (b & 3));
-      }
-      // two halves of four k-blocks (the second only for sides of more than 16 nodes):
-      // the reads of a half issue together
-#pragma unroll
-      for (int hb = 0; hb < 2; ++hb) {
-        if (hb == 0 || KB > 4) {
-          float z0a[4], z0b[4], a0v[4], a1v[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int b = 4 * hb + i;
-            const float *w0 = sW0 + (t8[b] == 63u ? (uint32_t)d_in : t8[b]) * FH1 + j;
-            z0a[i] = w0[0];
-            z0b[i] = w0[16];
-            const int ab = abase0 + s * NC * RS + 4 * b;
-            a0v[i] = W[ab];
-            a1v[i] = W[ab + 16 * RS];
+      // ================= forward: ik1 · P1 = Â Z0 + ik1 b0 =================
+      uint32_t tyA[2][2];     // [s][tile]: types of node rows 4g+r, 6 bits; 63 = dropped/absent
+      f4 d1[2][2][2];         // [s][to][f]: P1, then D1 in place
+  #pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int KB = s ? KB1 : KB0, T = s ? T1 : T0;
+        const uint32_t kms = km0[s];
+        uint32_t tp[2] = {0u, 0u};
+  #pragma unroll
+        for (int to = 0; to < 2; ++to) {
+          d1[s][to][0] = f4{b0v0, b0v0, b0v0, b0v0};
+          d1[s][to][1] = f4{b0v1, b0v1, b0v1, b0v1};
+        }
+  #if SG32_HOIST_P1
+        // types, W0 rows and Â fragments of all eight k-blocks first (unconditional reads,
+        // two dependent LDS round trips per side instead of two per k-block): nodes past N
+        // are masked (k0 = 0 -> the zero row d_in), Â is zero there
+        uint32_t t8[8];
+  #pragma unroll
+        for (int b = 0; b < 8; ++b) t8[b] = (uint32_t)ty[s * NC + 4 * b + g];
+  #pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const uint32_t t_ = min(t8[b], (uint32_t)(d_in - 1));
+          const uint32_t k0 = (kms >> (4 * b + g)) & 1u;
+          t8[b] = k0 ? t_ : 63u;   // 63: dropped / absent (the W0 row read is d_in's zero row)
+          tp[b >> 2] |= t8[b] << (6 * (b & 3));
+        }
+        // two halves of four k-blocks (the second only for sides of more than 16 nodes):
+        // the reads of a half issue together
+  #pragma unroll
+        for (int hb = 0; hb < 2; ++hb) {
+          if (hb < T) {   // the second half only for sides of two tiles (KB > 4)
+            float z0a[4], z0b[4], a0v[4], a1v[4];
+  #pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int b = 4 * hb + i;
+              const float *w0 = sW0 + (t8[b] == 63u ? (uint32_t)d_in : t8[b]) * FH1 + j;
+              z0a[i] = w0[0];
+              z0b[i] = w0[16];
+              const int ab = abase0 + s * NC * RS + 4 * b;
+              a0v[i] = W[ab];
+              a1v[i] = W[ab + 16 * RS];
+            }
+  #pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int b = 4 * hb + i;
+              if (kb_live(b, T, KB)) {
+                d1[s][0][0] = mfma4(a0v[i], z0a[i], d1[s][0][0]);
+                d1[s][0][1] = mfma4(a0v[i], z0b[i], d1[s][0][1]);
+                if (T > 1) {
+                  d1[s][1][0] = mfma4(a1v[i], z0a[i], d1[s][1][0]);
+                  d1[s][1][1] = mfma4(a1v[i], z0b[i], d1[s][1][1]);
+                }
+              }
+            }
           }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int b = 4 * hb + i;
-            if (b < KB) {
-              d1[s][0][0] = mfma4(a0v[i], z0a[i], d1[s][0][0]);
-              d1[s][0][1] = mfma4(a0v[i], z0b[i], d1[s][0][1]);
-              if (T > 1) {
-                d1[s][1][0] = mfma4(a1v[i], z0a[i], d1[s][1][0]);
-                d1[s][1][1] = mfma4(a1v[i], z0b[i], d1[s][1][1]);
+        }
+  #else
+  #pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          if (kb_live(b, T, KB)) {
+            const int n = 4 * b + g;
+            uint32_t t_ = (uint32_t)ty[s * NC + n];
+            t_ = min(t_, (uint32_t)(d_in - 1));
+            const uint32_t k0 = (kms >> n) & 1u;
+            tp[b >> 2] |= (k0 ? t_ : 63u) << (6 * (b & 3));
+            const float *w0 = sW0 + (k0 ? t_ : (uint32_t)d_in) * FH1 + j;
+            const float z0a = w0[0], z0b = w0[16];
+            const int ab = abase0 + s * NC * RS + 4 * b;
+            const float a0 = W[ab];
+            d1[s][0][0] = mfma4(a0, z0a, d1[s][0][0]);
+            d1[s][0][1] = mfma4(a0, z0b, d1[s][0][1]);
+            if (T > 1) {
+              const float a1 = W[ab + 16 * RS];
+              d1[s][1][0] = mfma4(a1, z0a, d1[s][1][0]);
+              d1[s][1][1] = mfma4(a1, z0b, d1[s][1][1]);
+            }
+          } else {
+            tp[b >> 2] |= 63u << (6 * (b & 3));
+          }
+        }
+  #endif
+        tyA[s][0] = tp[0];
+        tyA[s][1] = tp[1];
+      }
+      // D1 = dropout(ik1 relu(P1)): one hash per element (node 16to+4r+g, feature 16f+j)
+      // gives both sides' draws; k-blocks past a side's nodes are zeroed
+  #pragma unroll
+      for (int to = 0; to < 2; ++to)
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nb = 4 * to + r;
+  #pragma unroll
+          for (int f = 0; f < 2; ++f) {
+            if (to < TM && nb < KBm) {
+              const uint32_t h =
+                  sg_mix((pk ^ ((1u << 26) | (uint32_t)(512 * to + 128 * r + 16 * f))) ^ lb1);
+  #pragma unroll
+              for (int s = 0; s < 2; ++s) {
+                const uint32_t dr = s ? (h >> 16) : (h & 0xFFFFu);
+                const float v = fmaxf(d1[s][to][f][r], 0.f);
+                d1[s][to][f][r] = (nb < (s ? KB1 : KB0) && dr < A.thr1) ? v : 0.f;
+              }
+            } else {
+              d1[0][to][f][r] = d1[1][to][f][r] = 0.f;
+            }
+          }
+        }
+
+      // Z1 = D1 W1 (D1 transposed through the tile), H2 = Â Z1 + b1, per side
+      f4 h2[2][2];
+  #pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int KB = s ? KB1 : KB0, T = s ? T1 : T0;
+  #pragma unroll
+        for (int to = 0; to < 2; ++to) {
+          if (to < T) {
+  #pragma unroll
+            for (int f = 0; f < 2; ++f)
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) sT[(16 * to + 4 * g + r) * TS1 + 16 * f + j] = d1[s][to][f][r];
+          }
+        }
+        sg_wsync();
+        f4 z1[2];
+        const f4 wlo = *(const f4 *)w1bp, whi = *(const f4 *)(w1bp + 4);
+  #pragma unroll
+        for (int to = 0; to < 2; ++to) {
+          z1[to] = f4{0.f, 0.f, 0.f, 0.f};
+          if (to < T) {
+            const float *Tr = sT + (16 * to + j) * TS1 + 8 * g;
+            const f4 lo = *(const f4 *)Tr, hi = *(const f4 *)(Tr + 4);
+  #pragma unroll
+            for (int qq = 0; qq < 4; ++qq) z1[to] = mfma4(lo[qq], wlo[qq], z1[to]);
+  #pragma unroll
+            for (int qq = 0; qq < 4; ++qq) z1[to] = mfma4(hi[qq], whi[qq], z1[to]);
+          }
+        }
+        float af[2][8];
+        load_af(s, T, KB, af);
+  #pragma unroll
+        for (int to = 0; to < 2; ++to) {
+          h2[s][to] = f4{b1v, b1v, b1v, b1v};
+          if (to < T) {
+  #pragma unroll
+            for (int b = 0; b < 8; ++b)
+              if (kb_live(b, T, KB)) h2[s][to] = mfma4(af[to][b], z1[b >> 2][b & 3], h2[s][to]);
+          }
+        }
+        sg_wsync();   // the tile is rewritten by the next side
+      }
+
+      // D2 = dropout(H2); zpre = D2·Wd + bd; x = dropout(pad(relu(zpre)))
+      float xo[2][8], d2[2][8];   // [s][4 to + r] ↔ node 16 to + 4 r + g
+      uint32_t kb2[2] = {0u, 0u};
+  #pragma unroll
+      for (int nb = 0; nb < 8; ++nb) {
+        const int to = nb >> 2, r = nb & 3;
+        if (to < TM && nb < KBm) {
+          const uint32_t h = sg_mix((pk ^ ((2u << 26) | (uint32_t)(256 * to + 64 * r))) ^ lb2);
+  #pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            if (nb < (s ? KB1 : KB0)) {
+              const bool k2 = (s ? (h >> 16) : (h & 0xFFFFu)) < A.thr2;
+              d2[s][nb] = k2 ? h2[s][to][r] : 0.f;   // D2 / ik2
+              kb2[s] |= (k2 ? 1u : 0u) << nb;
+              const float z = row_sum16(d2[s][nb] * wdv) + bd;
+              const bool k4 = (km4[s] >> (16 * to + 4 * r + g)) & 1u;   // includes n < N
+              xo[s][nb] = ((z > 0.f) & k4) ? z * A.ik4 : 0.f;
+            } else {
+              d2[s][nb] = xo[s][nb] = 0.f;
+            }
+          }
+        } else {
+          d2[0][nb] = d2[1][nb] = xo[0][nb] = xo[1][nb] = 0.f;
+        }
+      }
+      if (j == 0) {   // x1 | x2 for every lane (node 16to+4r+g of row group g)
+  #pragma unroll
+        for (int nb = 0; nb < 8; ++nb) {
+          sX[4 * nb + g] = xo[0][nb];
+          sX[NC + 4 * nb + g] = xo[1][nb];
+        }
+      }
+      sg_wsync();
+
+      // ================= NTN head (layers.py:282-310) =================
+      // lane (g, k = j) owns rows a = 4r' + g.  Per 4-column block bq of b (outer loop):
+      // u[r'] += Σ_b W[a][b][k] x2[b] (forward), and the partials Σ_{own a} x1[a] W[a][b][k]
+      // of ge2 = Σ_a x1[a] W[a][b][k] gm[k] share the Wa reads; the partials of the
+      // block are reduce-scattered over the four row groups at once (half 0 = g < 2
+      // keeps b % 4 < 2, then row g keeps b % 4 == g): cs[bq] ↔ b = 4 bq + g.
+      float u[8], cs[8];
+  #pragma unroll
+      for (int rr = 0; rr < 8; ++rr) u[rr] = cs[rr] = 0.f;
+  #ifdef SG32_ABL_NONTN   // timing ablation only (results invalid): no NTN W products
+      constexpr int NTN_BQ = 0;
+  #else
+      constexpr int NTN_BQ = 8;
+  #endif
+      // The Wa rows of one column block are read together (one LDS round trip per block):
+      // KR rows, KB0 rounded up to even, as straight-line code per KR.  Rows KB0..KR-1 of
+      // x1 are zero, so their u rows go unused and their cb terms are exact fmaf(0, w, cb).
+      auto ntn_fwd = [&](auto KRc) __attribute__((always_inline)) {
+        constexpr int KR = decltype(KRc)::value;
+  #pragma unroll
+        for (int bq = 0; bq < NTN_BQ; ++bq) {
+          if (kb_live(bq, T1, KB1)) {
+            const f4 x2 = *(const f4 *)(sX + NC + 4 * bq);
+            const float *wb = sWa + walane + ((4 * bq) ^ wswz);
+            f4 w[KR];
+  #pragma unroll
+            for (int rr = 0; rr < KR; ++rr) w[rr] = *(const f4 *)(wb + rr * 4 * FK * WAS);   // rows a >= D are zero
+            float cb[4] = {0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+            for (int rr = 0; rr < KR; ++rr) {
+              const float x1a = xo[0][rr];
+  #pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                u[rr] = fmaf(w[rr][e], x2[e], u[rr]);
+                cb[e] = fmaf(x1a, w[rr][e], cb[e]);
+              }
+            }
+            float hs[2];
+  #pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(cb[e]),
+                                                                __float_as_uint(cb[e + 2]), false, false);
+              hs[e] = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+            }
+            const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(hs[0]),
+                                                              __float_as_uint(hs[1]), false, false);
+            cs[bq] = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+          }
+        }
+      };
+  #if SG32_NTN_KR
+      if constexpr (T0 == 2) {
+        if (KB0 > 6) ntn_fwd(std::integral_constant<int, 8>{});
+        else ntn_fwd(std::integral_constant<int, 6>{});
+      } else {
+        if (KB0 > 2) ntn_fwd(std::integral_constant<int, 4>{});
+        else ntn_fwd(std::integral_constant<int, 2>{});
+      }
+  #else
+      ntn_fwd(std::integral_constant<int, 8>{});   // (KR = 8: every row read)
+  #endif
+  #if SG32_V_HOIST >= 1
+      // V entries of the lane's rows, read unconditionally (one LDS round trip; rows past
+      // the sides' k-blocks are never used): vu = u + V[k][a] (forward and ∂L/∂x1)
+      float vu[8], vb[8];
+  #pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        const int a = 4 * rr + g;
+        const int ac = a < D ? a : 0;
+        vu[rr] = u[rr] + sV[kc * VS + ac];
+        vb[rr] = sV[kc * VS + D + ac];
+      }
+      float mpart = 0.f;
+  #pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        if (kb_live(rr, T0, KB0)) mpart = fmaf(xo[0][rr], vu[rr], mpart);
+        if (kb_live(rr, T1, KB1)) mpart = fmaf(xo[1][rr], vb[rr], mpart);
+      }
+  #else
+      float mpart = 0.f;
+  #pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        if (kb_live(rr, T0, KB0)) {
+          const int a = 4 * rr + g;
+          const int ac = a < D ? a : 0;
+          mpart = fmaf(xo[0][rr], u[rr] + sV[kc * VS + ac], mpart);
+        }
+        if (kb_live(rr, T1, KB1)) {
+          const int b = 4 * rr + g;
+          const int bc = b < D ? b : 0;
+          mpart = fmaf(xo[1][rr], sV[kc * VS + D + bc], mpart);
+        }
+      }
+  #endif
+      const float m = xsum32(xsum16(mpart)) + bnk;
+      const float rk = (kv & (m > 0.f)) ? m : 0.f;
+      const float rsum = row_sum16(rk);
+      const float sv = INTENDED ? row_sum16(Uk * rk) : usum * rsum;
+      if (!BWD) {
+        if (l == 0) A.s_out[p] = sv;
+        return;
+      }
+      if (A.s_out && l == 0) A.s_out[p] = sv;
+      const float yhat = __expf(-A.yeta * sv * sv);
+      float gy;
+      if (!ALIGNED) {
+        gy = yhat - ybar;
+        lossa += 0.5f * gy * gy;
+      } else {
+        const float dl = yhat - label;
+        gy = dl * A.inv_batch;
+        lossa += 0.5f * dl * dl * A.inv_batch;
+      }
+      const float gs = gy * (-2.f * A.yeta * sv * yhat);
+
+      // ================= NTN backward =================
+      const float gmk = (kv & (m > 0.f)) ? (INTENDED ? gs * Uk : gs * usum) : 0.f;
+      if (g == 0) gUa += INTENDED ? gs * rk : gs * rsum;
+      // deferred NTN gradients: this pair's (x1 | 1, x2 | 1, gm)
+      {
+        float *nb_ = A.ntn + (size_t)(uint32_t)p * NBUF;
+        nb_[l] = ((l & (NC - 1)) == D) ? 1.f : sX[l];
+        if (g == 0) nb_[2 * NC + j] = gmk;
+      }
+      const float gmk4 = gmk * A.ik4;
+  #if SG32_V_HOIST >= 2
+      // the V entries of side 1's rows read unconditionally (one LDS round trip)
+      float vb2[8];
+  #pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        const int b = 4 * rr + g;
+        vb2[rr] = sV[kc * VS + D + (b < D ? b : 0)];
+      }
+  #endif
+      float ge[2][8];   // dL/dx · ik4 (before the x > 0 mask) of the lane's rows
+  #pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        ge[0][rr] = ge[1][rr] = 0.f;
+        if (kb_live(rr, T0, KB0)) {
+  #if SG32_V_HOIST >= 1
+          ge[0][rr] = row_sum16(gmk4 * vu[rr]);
+  #else
+          const int a = 4 * rr + g;
+          const int ac = a < D ? a : 0;
+          ge[0][rr] = row_sum16(gmk4 * (sV[kc * VS + ac] + u[rr]));
+  #endif
+        }
+      }
+  #pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        if (kb_live(rr, T1, KB1)) {
+  #if SG32_V_HOIST >= 2
+          ge[1][rr] = row_sum16(gmk4 * (vb2[rr] + cs[rr]));
+  #else
+          const int b = 4 * rr + g;
+          const int bc = b < D ? b : 0;
+          ge[1][rr] = row_sum16(gmk4 * (sV[kc * VS + D + bc] + cs[rr]));
+  #endif
+        }
+      }
+
+      // ================= GCN backward, per side =================
+  #pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int KB = s ? KB1 : KB0, T = s ? T1 : T0;
+        float af[2][8];
+        load_af(s, T, KB, af);
+        f4 gh2[2];
+  #pragma unroll
+        for (int to = 0; to < 2; ++to) {
+          gh2[to] = f4{0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int nb = 4 * to + r;
+            if (kb_live(nb, T, KB)) {
+              const float gp = xo[s][nb] > 0.f ? ge[s][nb] : 0.f;
+              gwda = fmaf(d2[s][nb], gp, gwda);
+              gbda += gp;
+              const float v = ((kb2[s] >> nb) & 1u) ? gp * wdv : 0.f;
+              gb1a += v;
+              gh2[to][r] = v;
+            }
+          }
+        }
+        // gZ1 = Âᵀ gH2 (Â symmetric) in both orientations
+        f4 gz1[2], gz1t[2];
+  #pragma unroll
+        for (int to = 0; to < 2; ++to) {
+          gz1[to] = gz1t[to] = f4{0.f, 0.f, 0.f, 0.f};
+          if (to < T) {
+  #pragma unroll
+            for (int b = 0; b < 8; ++b) {
+              if (kb_live(b, T, KB)) {
+                gz1[to] = mfma4(af[to][b], gh2[b >> 2][b & 3], gz1[to]);
+                gz1t[to] = mfma4(gh2[b >> 2][b & 3], af[to][b], gz1t[to]);
+              }
+            }
+          }
+        }
+        // gW1 += D1ᵀ gZ1 (D1's C-layout entries are the A operand)
+  #pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          if (kb_live(b, T, KB)) {
+  #pragma unroll
+            for (int f = 0; f < 2; ++f) gw1[f] = mfma4(d1[s][b >> 2][f][b & 3], gz1[b >> 2][b & 3], gw1[f]);
+          }
+        }
+        // gD1 · ik1 = gZ1 (W1 ik1)ᵀ; gP1 = keep·relu' (D1 > 0); gZ0 = Âᵀ gP1
+        f4 gp1[2][2];   // [to][f]
+  #pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const f4 wt = *(const f4 *)(w1tp + 16 * f * W1S);
+  #pragma unroll
+          for (int to = 0; to < 2; ++to) {
+            gp1[to][f] = f4{0.f, 0.f, 0.f, 0.f};
+            if (to < T) {
+              f4 acc = {0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+              for (int qq = 0; qq < 4; ++qq) acc = mfma4(gz1t[to][qq], wt[qq], acc);
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) gp1[to][f][r] = d1[s][to][f][r] > 0.f ? acc[r] : 0.f;
+              const float gsum = (gp1[to][f][0] + gp1[to][f][1]) + (gp1[to][f][2] + gp1[to][f][3]);
+              if (f) gb0a1 += gsum;
+              else gb0a0 += gsum;
+            }
+          }
+        }
+  #pragma unroll
+        for (int to = 0; to < 2; ++to) {
+          if (to < T) {
+            // one-hot Xᵀ rows: type 16τ + j, k-slots 8g + e ↔ node rows 4g + (e & 3)
+            uint4 ohA[2], ohL[2];
+  #pragma unroll
+            for (int tau = 0; tau < 2; ++tau) {
+              uint32_t o[4];
+  #pragma unroll
+              for (int r = 0; r < 4; ++r)
+                o[r] = (((tyA[s][to] >> (6 * r)) & 63u) == (uint32_t)(16 * tau + j)) ? 0x3F80u : 0u;
+              const uint32_t o01 = o[0] | (o[1] << 16), o23 = o[2] | (o[3] << 16);
+              ohA[tau] = uint4{o01, o23, o01, o23};
+              ohL[tau] = uint4{o01, o23, 0u, 0u};
+            }
+  #pragma unroll
+            for (int f = 0; f < 2; ++f) {
+              f4 gz0 = {0.f, 0.f, 0.f, 0.f};
+  #pragma unroll
+              for (int b = 0; b < 8; ++b)
+                if (kb_live(b, T, KB)) gz0 = mfma4(af[to][b], gp1[b >> 2][f][b & 3], gz0);
+              uint32_t h01, m01, l01, h23, m23, l23;
+              split3(gz0[0], gz0[1], h01, m01, l01);
+              split3(gz0[2], gz0[3], h23, m23, l23);
+              const uint4 bhm = {h01, h23, m01, m23}, bl = {l01, l23, 0u, 0u};
+  #pragma unroll
+              for (int tau = 0; tau < 2; ++tau) {
+                gw0[tau][f] = mfbf(ohL[tau], bl, gw0[tau][f]);
+                gw0[tau][f] = mfbf(ohA[tau], bhm, gw0[tau][f]);
               }
             }
           }
         }
       }
-#else
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        if (b < KB) {
-          const int n = 4 * b + g;
-          uint32_t t_ = (uint32_t)ty[s * NC + n];
-          t_ = min(t_, (uint32_t)(d_in - 1));
-          const uint32_t k0 = (kms >> n) & 1u;
-          tp[b >> 2] |= (k0 ? t_ : 63u) << (6 * (b & 3));
-          const float *w0 = sW0 + (k0 ? t_ : (uint32_t)d_in) * FH1 + j;
-          const float z0a = w0[0], z0b = w0[16];
-          const int ab = abase0 + s * NC * RS + 4 * b;
-          const float a0 = W[ab];
-          d1[s][0][0] = mfma4(a0, z0a, d1[s][0][0]);
-          d1[s][0][1] = mfma4(a0, z0b, d1[s][0][1]);
-          if (T > 1) {
-            const float a1 = W[ab + 16 * RS];
-            d1[s][1][0] = mfma4(a1, z0a, d1[s][1][0]);
-            d1[s][1][1] = mfma4(a1, z0b, d1[s][1][1]);
-          }
-        } else {
-          tp[b >> 2] |= 63u << (6 * (b & 3));
-        }
-      }
-#endif
-      tyA[s][0] = tp[0];
-      tyA[s][1] = tp[1];
-    }
-    // D1 = dropout(ik1 relu(P1)): one hash per element (node 16to+4r+g, feature 16f+j)
-    // gives both sides' draws; k-blocks past a side's nodes are zeroed
-#pragma unroll
-    for (int to = 0; to < 2; ++to)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int nb = 4 * to + r;
-#pragma unroll
-        for (int f = 0; f < 2; ++f) {
-          if (nb < KBm) {
-            const uint32_t h =
-                sg_mix((pk ^ ((1u << 26) | (uint32_t)(512 * to + 128 * r + 16 * f))) ^ lb1);
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-              const uint32_t dr = s ? (h >> 16) : (h & 0xFFFFu);
-              const float v = fmaxf(d1[s][to][f][r], 0.f);
-              d1[s][to][f][r] = (nb < (s ? KB1 : KB0) && dr < A.thr1) ? v : 0.f;
-            }
-          } else {
-            d1[0][to][f][r] = d1[1][to][f][r] = 0.f;
-          }
-        }
-      }
-
-    // Z1 = D1 W1 (D1 transposed through the tile), H2 = Â Z1 + b1, per side
-    f4 h2[2][2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int KB = s ? KB1 : KB0, T = s ? T1 : T0;
-#pragma unroll
-      for (int to = 0; to < 2; ++to) {
-        if (to < T) {
-#pragma unroll
-          for (int f = 0; f < 2; ++f)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sT[(16 * to + 4 * g + r) * TS1 + 16 * f + j] = d1[s][to][f][r];
-        }
-      }
-      sg_wsync();
-      f4 z1[2];
-      const f4 wlo = *(const f4 *)w1bp, whi = *(const f4 *)(w1bp + 4);
-#pragma unroll
-      for (int to = 0; to < 2; ++to) {
-        z1[to] = f4{0.f, 0.f, 0.f, 0.f};
-        if (to < T) {
-          const float *Tr = sT + (16 * to + j) * TS1 + 8 * g;
-          const f4 lo = *(const f4 *)Tr, hi = *(const f4 *)(Tr + 4);
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) z1[to] = mfma4(lo[qq], wlo[qq], z1[to]);
-#pragma unroll
-          for (int qq = 0; qq < 4; ++qq) z1[to] = mfma4(hi[qq], whi[qq], z1[to]);
-        }
-      }
-      float af[2][8];
-      load_af(s, T, KB, af);
-#pragma unroll
-      for (int to = 0; to < 2; ++to) {
-        h2[s][to] = f4{b1v, b1v, b1v, b1v};
-        if (to < T) {
-#pragma unroll
-          for (int b = 0; b < 8; ++b)
-            if (b < KB) h2[s][to] = mfma4(af[to][b], z1[b >> 2][b & 3], h2[s][to]);
-        }
-      }
-      sg_wsync();   // the tile is rewritten by the next side
-    }
-
-    // D2 = dropout(H2); zpre = D2·Wd + bd; x = dropout(pad(relu(zpre)))
-    float xo[2][8], d2[2][8];   // [s][4 to + r] ↔ node 16 to + 4 r + g
-    uint32_t kb2[2] = {0u, 0u};
-#pragma unroll
-    for (int nb = 0; nb < 8; ++nb) {
-      const int to = nb >> 2, r = nb & 3;
-      if (nb < KBm) {
-        const uint32_t h = sg_mix((pk ^ ((2u << 26) | (uint32_t)(256 * to + 64 * r))) ^ lb2);
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          if (nb < (s ? KB1 : KB0)) {
-            const bool k2 = (s ? (h >> 16) : (h & 0xFFFFu)) < A.thr2;
-            d2[s][nb] = k2 ? h2[s][to][r] : 0.f;   // D2 / ik2
-            kb2[s] |= (k2 ? 1u : 0u) << nb;
-            const float z = row_sum16(d2[s][nb] * wdv) + bd;
-            const bool k4 = (km4[s] >> (16 * to + 4 * r + g)) & 1u;   // includes n < N
-            xo[s][nb] = ((z > 0.f) & k4) ? z * A.ik4 : 0.f;
-          } else {
-            d2[s][nb] = xo[s][nb] = 0.f;
-          }
-        }
-      } else {
-        d2[0][nb] = d2[1][nb] = xo[0][nb] = xo[1][nb] = 0.f;
-      }
-    }
-    if (j == 0) {   // x1 | x2 for every lane (node 16to+4r+g of row group g)
-#pragma unroll
-      for (int nb = 0; nb < 8; ++nb) {
-        sX[4 * nb + g] = xo[0][nb];
-        sX[NC + 4 * nb + g] = xo[1][nb];
-      }
-    }
-    sg_wsync();
-
-    // ================= NTN head (layers.py:282-310) =================
-    // lane (g, k = j) owns rows a = 4r' + g.  Per 4-column block bq of b (outer loop):
-    // u[r'] += Σ_b W[a][b][k] x2[b] (forward), and the partials Σ_{own a} x1[a] W[a][b][k]
-    // of ge2 = Σ_a x1[a] W[a][b][k] gm[k] share the Wa reads; the partials of the
-    // block are reduce-scattered over the four row groups at once (half 0 = g < 2
-    // keeps b % 4 < 2, then row g keeps b % 4 == g): cs[bq] ↔ b = 4 bq + g.
-    float u[8], cs[8];
-#pragma unroll
-    for (int rr = 0; rr < 8; ++rr) u[rr] = cs[rr] = 0.f;
-#ifdef SG32_ABL_NONTN   // timing ablation only (results invalid): no NTN W products
-    constexpr int NTN_BQ = 0;
-#else
-    constexpr int NTN_BQ = 8;
-#endif
-    // The Wa rows of one column block are read together (one LDS round trip per block):
-    // KR rows, KB0 rounded up to even, as straight-line code per KR.  Rows KB0..KR-1 of
-    // x1 are zero, so their u rows go unused and their cb terms are exact fmaf(0, w, cb).
-    auto ntn_fwd = [&](auto KRc) __attribute__((always_inline)) {
-      constexpr int KR = decltype(KRc)::value;
-#pragma unroll
-      for (int bq = 0; bq < NTN_BQ; ++bq) {
-        if (bq < KB1) {
-          const f4 x2 = *(const f4 *)(sX + NC + 4 * bq);
-          const float *wb = sWa + walane + ((4 * bq) ^ wswz);
-          f4 w[KR];
-#pragma unroll
-          for (int rr = 0; rr < KR; ++rr) w[rr] = *(const f4 *)(wb + rr * 4 * FK * WAS);   // rows a >= D are zero
-          float cb[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int rr = 0; rr < KR; ++rr) {
-            const float x1a = xo[0][rr];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              u[rr] = fmaf(w[rr][e], x2[e], u[rr]);
-              cb[e] = fmaf(x1a, w[rr][e], cb[e]);
-            }
-          }
-          float hs[2];
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(cb[e]),
-                                                              __float_as_uint(cb[e + 2]), false, false);
-            hs[e] = __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
-          }
-          const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(hs[0]),
-                                                            __float_as_uint(hs[1]), false, false);
-          cs[bq] = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
-        }
-      }
     };
-#if SG32_NTN_KR
-    if (KB0 > 6) ntn_fwd(std::integral_constant<int, 8>{});
-    else if (KB0 > 4) ntn_fwd(std::integral_constant<int, 6>{});
-    else if (KB0 > 2) ntn_fwd(std::integral_constant<int, 4>{});
-    else ntn_fwd(std::integral_constant<int, 2>{});
-#else
-    ntn_fwd(std::integral_constant<int, 8>{});   // (KR = 8: every row read)
-#endif
-#if SG32_V_HOIST >= 1
-    // V entries of the lane's rows, read unconditionally (one LDS round trip; rows past
-    // the sides' k-blocks are never used): vu = u + V[k][a] (forward and ∂L/∂x1)
-    float vu[8], vb[8];
-#pragma unroll
-    for (int rr = 0; rr < 8; ++rr) {
-      const int a = 4 * rr + g;
-      const int ac = a < D ? a : 0;
-      vu[rr] = u[rr] + sV[kc * VS + ac];
-      vb[rr] = sV[kc * VS + D + ac];
-    }
-    float mpart = 0.f;
-#pragma unroll
-    for (int rr = 0; rr < 8; ++rr) {
-      if (rr < KB0) mpart = fmaf(xo[0][rr], vu[rr], mpart);
-      if (rr < KB1) mpart = fmaf(xo[1][rr], vb[rr], mpart);
-    }
-#else
-    float mpart = 0.f;
-#pragma unroll
-    for (int rr = 0; rr < 8; ++rr) {
-      if (rr < KB0) {
-        const int a = 4 * rr + g;
-        const int ac = a < D ? a : 0;
-        mpart = fmaf(xo[0][rr], u[rr] + sV[kc * VS + ac], mpart);
-      }
-      if (rr < KB1) {
-        const int b = 4 * rr + g;
-        const int bc = b < D ? b : 0;
-        mpart = fmaf(xo[1][rr], sV[kc * VS + D + bc], mpart);
-      }
-    }
-#endif
-    const float m = xsum32(xsum16(mpart)) + bnk;
-    const float rk = (kv & (m > 0.f)) ? m : 0.f;
-    const float rsum = row_sum16(rk);
-    const float sv = INTENDED ? row_sum16(Uk * rk) : usum * rsum;
-    if (!BWD) {
-      if (l == 0) A.s_out[p] = sv;
-      continue;
-    }
-    if (A.s_out && l == 0) A.s_out[p] = sv;
-    const float yhat = __expf(-A.yeta * sv * sv);
-    float gy;
-    if (!ALIGNED) {
-      gy = yhat - ybar;
-      lossa += 0.5f * gy * gy;
+    const bool two0 = N0 > 16, two1 = N1 > 16;
+    if (two0) {
+      if (two1) body(std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{});
+      else body(std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{});
     } else {
-      const float dl = yhat - label;
-      gy = dl * A.inv_batch;
-      lossa += 0.5f * dl * dl * A.inv_batch;
-    }
-    const float gs = gy * (-2.f * A.yeta * sv * yhat);
-
-    // ================= NTN backward =================
-    const float gmk = (kv & (m > 0.f)) ? (INTENDED ? gs * Uk : gs * usum) : 0.f;
-    if (g == 0) gUa += INTENDED ? gs * rk : gs * rsum;
-    // deferred NTN gradients: this pair's (x1 | 1, x2 | 1, gm)
-    {
-      float *nb_ = A.ntn + (size_t)(uint32_t)p * NBUF;
-      nb_[l] = ((l & (NC - 1)) == D) ? 1.f : sX[l];
-      if (g == 0) nb_[2 * NC + j] = gmk;
-    }
-    const float gmk4 = gmk * A.ik4;
-#if SG32_V_HOIST >= 2
-    // the V entries of side 1's rows read unconditionally (one LDS round trip)
-    float vb2[8];
-#pragma unroll
-    for (int rr = 0; rr < 8; ++rr) {
-      const int b = 4 * rr + g;
-      vb2[rr] = sV[kc * VS + D + (b < D ? b : 0)];
-    }
-#endif
-    float ge[2][8];   // dL/dx · ik4 (before the x > 0 mask) of the lane's rows
-#pragma unroll
-    for (int rr = 0; rr < 8; ++rr) {
-      ge[0][rr] = ge[1][rr] = 0.f;
-      if (rr < KB0) {
-#if SG32_V_HOIST >= 1
-        ge[0][rr] = row_sum16(gmk4 * vu[rr]);
-#else
-        const int a = 4 * rr + g;
-        const int ac = a < D ? a : 0;
-        ge[0][rr] = row_sum16(gmk4 * (sV[kc * VS + ac] + u[rr]));
-#endif
-      }
-    }
-#pragma unroll
-    for (int rr = 0; rr < 8; ++rr) {
-      if (rr < KB1) {
-#if SG32_V_HOIST >= 2
-        ge[1][rr] = row_sum16(gmk4 * (vb2[rr] + cs[rr]));
-#else
-        const int b = 4 * rr + g;
-        const int bc = b < D ? b : 0;
-        ge[1][rr] = row_sum16(gmk4 * (sV[kc * VS + D + bc] + cs[rr]));
-#endif
-      }
-    }
-
-    // ================= GCN backward, per side =================
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int KB = s ? KB1 : KB0, T = s ? T1 : T0;
-      float af[2][8];
-      load_af(s, T, KB, af);
-      f4 gh2[2];
-#pragma unroll
-      for (int to = 0; to < 2; ++to) {
-        gh2[to] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int nb = 4 * to + r;
-          if (nb < KB) {
-            const float gp = xo[s][nb] > 0.f ? ge[s][nb] : 0.f;
-            gwda = fmaf(d2[s][nb], gp, gwda);
-            gbda += gp;
-            const float v = ((kb2[s] >> nb) & 1u) ? gp * wdv : 0.f;
-            gb1a += v;
-            gh2[to][r] = v;
-          }
-        }
-      }
-      // gZ1 = Âᵀ gH2 (Â symmetric) in both orientations
-      f4 gz1[2], gz1t[2];
-#pragma unroll
-      for (int to = 0; to < 2; ++to) {
-        gz1[to] = gz1t[to] = f4{0.f, 0.f, 0.f, 0.f};
-        if (to < T) {
-#pragma unroll
-          for (int b = 0; b < 8; ++b) {
-            if (b < KB) {
-              gz1[to] = mfma4(af[to][b], gh2[b >> 2][b & 3], gz1[to]);
-              gz1t[to] = mfma4(gh2[b >> 2][b & 3], af[to][b], gz1t[to]);
-            }
-          }
-        }
-      }
-      // gW1 += D1ᵀ gZ1 (D1's C-layout entries are the A operand)
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        if (b < KB) {
-#pragma unroll
-          for (int f = 0; f < 2; ++f) gw1[f] = mfma4(d1[s][b >> 2][f][b & 3], gz1[b >> 2][b & 3], gw1[f]);
-        }
-      }
-      // gD1 · ik1 = gZ1 (W1 ik1)ᵀ; gP1 = keep·relu' (D1 > 0); gZ0 = Âᵀ gP1
-      f4 gp1[2][2];   // [to][f]
-#pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        const f4 wt = *(const f4 *)(w1tp + 16 * f * W1S);
-#pragma unroll
-        for (int to = 0; to < 2; ++to) {
-          gp1[to][f] = f4{0.f, 0.f, 0.f, 0.f};
-          if (to < T) {
-            f4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int qq = 0; qq < 4; ++qq) acc = mfma4(gz1t[to][qq], wt[qq], acc);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) gp1[to][f][r] = d1[s][to][f][r] > 0.f ? acc[r] : 0.f;
-            const float gsum = (gp1[to][f][0] + gp1[to][f][1]) + (gp1[to][f][2] + gp1[to][f][3]);
-            if (f) gb0a1 += gsum;
-            else gb0a0 += gsum;
-          }
-        }
-      }
-#pragma unroll
-      for (int to = 0; to < 2; ++to) {
-        if (to < T) {
-          // one-hot Xᵀ rows: type 16τ + j, k-slots 8g + e ↔ node rows 4g + (e & 3)
-          uint4 ohA[2], ohL[2];
-#pragma unroll
-          for (int tau = 0; tau < 2; ++tau) {
-            uint32_t o[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              o[r] = (((tyA[s][to] >> (6 * r)) & 63u) == (uint32_t)(16 * tau + j)) ? 0x3F80u : 0u;
-            const uint32_t o01 = o[0] | (o[1] << 16), o23 = o[2] | (o[3] << 16);
-            ohA[tau] = uint4{o01, o23, o01, o23};
-            ohL[tau] = uint4{o01, o23, 0u, 0u};
-          }
-#pragma unroll
-          for (int f = 0; f < 2; ++f) {
-            f4 gz0 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int b = 0; b < 8; ++b)
-              if (b < KB) gz0 = mfma4(af[to][b], gp1[b >> 2][f][b & 3], gz0);
-            uint32_t h01, m01, l01, h23, m23, l23;
-            split3(gz0[0], gz0[1], h01, m01, l01);
-            split3(gz0[2], gz0[3], h23, m23, l23);
-            const uint4 bhm = {h01, h23, m01, m23}, bl = {l01, l23, 0u, 0u};
-#pragma unroll
-            for (int tau = 0; tau < 2; ++tau) {
-              gw0[tau][f] = mfbf(ohL[tau], bl, gw0[tau][f]);
-              gw0[tau][f] = mfbf(ohA[tau], bhm, gw0[tau][f]);
-            }
-          }
-        }
-      }
+      if (two1) body(std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{});
+      else body(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
     }
   }
 

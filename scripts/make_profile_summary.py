@@ -75,6 +75,11 @@ if fk:
     traffic['same_run_ms_per_step'] = tb['ms_per_step']
     traffic['rocprof_over_event'] = float(fk[0]['AverageNs']) * 1e-6 / ev_ms
 traffic['tree'] = tag
+# the fused kernel's sources the counters belong to: bench.py reports these bytes only
+# while the tree's sources hash the same (a kernel change makes them stale)
+sys.path.insert(0, root)
+from bench import fused_kernel_source_hash  # noqa: E402
+traffic['sources_sha1'] = fused_kernel_source_hash()
 json.dump(traffic, open(os.path.join(dst, 'traffic.json'), 'w'), indent=1)
 
 mf = {}
