@@ -244,8 +244,13 @@ __device__ __forceinline__ int sg_order_key(const S &src, int64_t p, int nmax, i
   n0 = n0 < 0 ? 0 : (n0 > nmax ? nmax : n0);
   n1 = n1 < 0 ? 0 : (n1 > nmax ? nmax : n1);
   // fast: 1 = sg_fast: class (N0 > 8) + 2 (N1 > 8), the kernel's four (K0, K1) bodies
-  // (third Â k-step per side); 2 = sg_fast32 (k-blocks of 4 nodes)
-  if (fast == 2) return ((n0 + 3) >> 2) + ((n1 + 3) >> 2);
+  // (third Â k-step per side); 2 = sg_fast32: class-major, the tile-count class
+  // (N0 > 16) + 2 (N1 > 16) of its four (T0, T1) bodies, then the k-blocks of 4 nodes, so
+  // that a wave's consecutive pairs run one body and cost about the same
+  if (fast == 2) {
+    const int kb0 = (n0 + 3) >> 2, kb1 = (n1 + 3) >> 2;
+    return ((n0 > 16) + 2 * (n1 > 16)) * 17 + kb0 + kb1;
+  }
   return fast ? (n0 > 8) + 2 * (n1 > 8) : n0 + n1;
 }
 
@@ -599,7 +604,7 @@ int64_t sg_pair_order_workspace_bytes(const sg_model_t *model, int64_t n_pairs) 
 extern "C++" template <class S>
 static int32_t launch_order(S src, int nmax, int fast, int64_t n_pairs, int32_t *order_out,
                             void *workspace, hipStream_t st, int32_t *class_start = nullptr) {
-  const int K = fast == 1 ? 4 : (fast == 2 ? 2 * ((nmax + 3) / 4) + 1 : 2 * nmax + 1);
+  const int K = fast == 1 ? 4 : (fast == 2 ? 4 * 17 : 2 * nmax + 1);
   const int nb = (int)((n_pairs + kOrderChunk - 1) / kOrderChunk);
   int32_t *cnt = (int32_t *)workspace;
   hipLaunchKernelGGL(sg_order_count<S>, dim3(nb), dim3(256), 0, st, src, n_pairs, nmax, fast, K,

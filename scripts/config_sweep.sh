@@ -23,4 +23,6 @@ run c4_emu8 --dataset syn_aids10knef --emulate-world 8 --steps 3 --warmup 1 --cp
 run c5_n1 --dataset syn_web --steps 3 --warmup 1 --cpu-sample -1
 run c5_emu8 --dataset syn_web --emulate-world 8 --steps 3 --warmup 1 --cpu-sample -1
 run avg_n1 --stack average --cpu-sample -1
+run att_n1 --stack attention --cpu-sample -1
+run att_emu8 --stack attention --emulate-world 8 --steps 200 --warmup 20 --cpu-sample -1
 exit 0

@@ -62,6 +62,12 @@ def test_fast32_matches_generic_and_is_reproducible(gpu, monkeypatch):
     model.fwd_bwd(batch, seed=seed)
     assert torch.equal(g32, model.grad), 'fused32 fwd_bwd is not bitwise reproducible'
     model.balance(batch)
+    # the capacity-32 order: stable sort by the tile-count class (N0 > 16) + 2 (N1 > 16)
+    # of the kernel's (T0, T1) bodies, then by the k-blocks of 4 nodes
+    n = np.array([g.number_of_nodes() for g in prob.graphs])
+    n0, n1 = n[prob.pairs[:, 0]], n[prob.pairs[:, 1]]
+    key = ((n0 > 16).astype(int) + 2 * (n1 > 16)) * 17 + (n0 + 3) // 4 + (n1 + 3) // 4
+    assert np.array_equal(batch.order.cpu().numpy(), np.argsort(key, kind='stable'))
     assert np.array_equal(model.pred_sim_without_act(batch, seed=seed).cpu().numpy(), s32)
     model.fwd_bwd(batch, seed=seed)
     _check_grad(model.grad.cpu().numpy(), g32.cpu().numpy(), prob, tol=1e-5)
