@@ -11,7 +11,8 @@
 // compile only together with SG_TIMING_ABLATION_BUILD, which build.py never passes to
 // the product library (graphembedding_amd/lib/libsiamese_hip.so), so a hand build
 // with one ablation macro alone fails here instead of producing a silently wrong .so.
-#if (defined(SG32_ABL_NOREC) || defined(SG32_ABL_NONTN) || defined(SG_WEB_ABL_NOH2)) && \
+#if (defined(SG32_ABL_NOREC) || defined(SG32_ABL_NONTN) || defined(SG_WEB_ABL_NOH2) || \
+     defined(SG_WEB_ABL_FHASH) || defined(SG_WEB_ABL_FH1) || defined(SG_WEB_ABL_FH2)) && \
     !defined(SG_TIMING_ABLATION_BUILD)
 #error "timing ablation macro without SG_TIMING_ABLATION_BUILD: results would be invalid"
 #endif

@@ -588,6 +588,17 @@ __device__ __forceinline__ int2 web_unit_q(int u, const int32_t *isorted, const 
   return make_int2((u < n_units && s0 + kk < end) ? isorted[s0 + kk] : -1, gsz);
 }
 
+// the forward's keep draws (the backward reads them back, SG_WEB_MASKS); SG_WEB_ABL_FHASH
+// (timing ablation only, results invalid) replaces the hash by one compare
+__device__ __forceinline__ bool web_fkeep(uint32_t pk, uint32_t layer, uint32_t side, uint32_t e,
+                                          uint32_t thr) {
+#ifdef SG_WEB_ABL_FHASH
+  return ((pk ^ e ^ layer ^ side) & 0xFFFFu) < thr;
+#else
+  return sg_keep(pk, layer, side, e, thr);
+#endif
+}
+
 template <bool BWD, int NTB, bool LCSR>
 __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
   using ColT = typename std::conditional<LCSR, uint16_t, int>::type;
@@ -776,6 +787,9 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
         h[4 * c] = b.x; h[4 * c + 1] = b.y; h[4 * c + 2] = b.z; h[4 * c + 3] = b.w;
       }
       if (n < N) {
+#ifdef SG_WEB_ABL_FH1   // timing ablation only (results invalid): the forward skips the H1 gather
+        if (BWD)
+#endif
         csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
           const float *wr = sW0 + sEtk[mm] * W0S + 4 * g;
           const float4 wa = *(const float4 *)wr, wb = *(const float4 *)(wr + 16);
@@ -791,7 +805,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
             const int f = 16 * c + 4 * g + s;
             const float hv = h[4 * c + s] > 0.f ? h[4 * c + s] : 0.f;
             const bool k1 = use_mw ? ((mw[u] >> (4 * c + s)) & 1u) != 0u
-                                   : sg_keep(pk, 1, side, (uint32_t)(n * WH1 + f), A.thr1);
+                                   : web_fkeep(pk, 1, side, (uint32_t)(n * WH1 + f), A.thr1);
             if (!BWD) mw[u] |= (k1 ? 1u : 0u) << (4 * c + s);
             h[4 * c + s] = k1 ? hv : 0.f;
           }
@@ -836,6 +850,9 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
 #ifdef SG_WEB_ABL_NOH2   // timing ablation only (results invalid): the backward skips the H2 pass
         if (!BWD)
 #endif
+#ifdef SG_WEB_ABL_FH2   // timing ablation only (results invalid): the forward skips the H2 gather
+        if (BWD)
+#endif
         csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
           const float4 zz = *(const float4 *)(sZ1k + mm * ZS + 4 * g);
           h2[0] = fmaf(v, zz.x, h2[0]); h2[1] = fmaf(v, zz.y, h2[1]);
@@ -847,14 +864,14 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         k2[s] = use_mw ? ((mw[u] >> (8 + s)) & 1u) != 0u
-                       : sg_keep(pk, 2, side, (uint32_t)(n * WH2 + 4 * g + s), A.thr2);
+                       : web_fkeep(pk, 2, side, (uint32_t)(n * WH2 + 4 * g + s), A.thr2);
         if (!BWD) mw[u] |= (k2[s] ? 1u : 0u) << (8 + s);
         part = fmaf(k2[s] ? h2[s] : 0.f, sWd[4 * g + s], part);
       }
       const float pre = sgk::xsum32(sgk::xsum16(part)) + bd;
       const float z = pre > 0.f ? pre : 0.f;
       const bool k4 = n < N && (use_mw ? ((mw[u] >> 12) & 1u) != 0u
-                                       : sg_keep(pk, 4, side, (uint32_t)n, A.thr4));
+                                       : web_fkeep(pk, 4, side, (uint32_t)n, A.thr4));
       if (!BWD) {
         if (g == 0 && n < N)
           A.X[((int64_t)side * A.Cp + p) * A.Dp + n] = k4 ? z * A.ik4 : 0.f;
