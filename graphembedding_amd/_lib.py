@@ -155,6 +155,8 @@ def lib():
     L.sg_web_workspace_bytes.restype = c_i64
     L.sg_web_workspace_bytes_ex.argtypes = [pm, c_i64, c_i64]
     L.sg_web_workspace_bytes_ex.restype = c_i64
+    L.sg_web_release.argtypes = []
+    L.sg_web_release.restype = ctypes.c_int32
     L.sg_web_forward.argtypes = [pm, pc, vp, c_i64, c_i64, vp, c_u64, vp, vp, c_i64, vp]
     L.sg_web_forward.restype = c_i32
     L.sg_web_fwd_bwd.argtypes = [pm, pc, vp, vp, c_i64, c_i64, c_i64, vp, c_u64, vp, c_i32, vp,
@@ -181,7 +183,7 @@ EXPORTED_SYMBOLS = ('sg_version', 'sg_record_bytes', 'sg_record_bytes_ex', 'sg_m
                     'sg_forward_ex', 'sg_fwd_bwd_ex', 'sg_pair_order',
                     'sg_pair_order_workspace_bytes', 'sg_sampler_random', 'sg_sampler_density',
                     'sg_adam_workspace_bytes', 'sg_adam_tf_ex', 'sg_web_workspace_bytes',
-                    'sg_web_workspace_bytes_ex',
+                    'sg_web_workspace_bytes_ex', 'sg_web_release',
                     'sg_web_forward', 'sg_web_fwd_bwd', 'sg_fwd_bwd_dseed', 'sg_seed_advance',
                     'sg_feed_step', 'sg_pair_order_src', 'sg_forward_src', 'sg_fwd_bwd_src',
                     'sg_pair_order_cls', 'sg_forward_cls', 'sg_fwd_bwd_cls')
@@ -490,3 +492,11 @@ def web_fwd_bwd(m: SgModel, store: SgCsrStore, pairs, labels, n_pairs, pair_offs
                                int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(y_stats), int(add_label_term),
                                _ptr(s_out), _ptr(grad_out), _ptr(loss_out), _ptr(workspace),
                                int(chunk), _stream(stream)), 'sg_web_fwd_bwd')
+
+
+def web_release():
+    """sg_web_release: destroy the graph-store pipeline's auxiliary streams and events
+    (teardown; no sg_web_* call may be in flight)."""
+    rc = int(lib().sg_web_release())
+    if rc != 0:
+        raise SiameseHipError('sg_web_release failed ({})'.format(rc))

@@ -30,7 +30,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <type_traits>
+#include <vector>
 
 #include "sg_common.h"
 #include "sg_mfma.h"
@@ -2333,26 +2335,60 @@ int sg_web_lds_ok(const sg_model_t *m) {
 }
 
 // The chunk pipeline's second stream and its events (sg_web_run: F = a chunk's forward
-// instance kernel done, G[slot] = the GEMMs of the chunk in that workspace slot done),
-// created once per host thread and device
-static int web_aux(hipStream_t *gs, hipEvent_t *evF, hipEvent_t *evG) {
-  constexpr int kMaxDev = 64;
-  thread_local hipStream_t streams[kMaxDev] = {};
-  thread_local hipEvent_t evs[kMaxDev][3] = {};
+// instance kernel done, G[slot] = the GEMMs of the chunk in that workspace slot done), one
+// set per (device, caller stream): calls on different caller streams do not share a second
+// stream (no false dependency between them), and calls from any host thread on the same
+// caller stream reuse one set.  sg_web_release() destroys them all (teardown).
+struct WebAux {
+  int dev;
+  hipStream_t caller, aux;
+  hipEvent_t ev[3];
+};
+static std::mutex g_web_aux_mu;
+static std::vector<WebAux> g_web_aux;
+
+static int web_aux(hipStream_t caller, hipStream_t *gs, hipEvent_t *evF, hipEvent_t *evG) {
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return SG_ERR_HIP;
-  if (!streams[dev]) {
+  if (hipGetDevice(&dev) != hipSuccess) return SG_ERR_HIP;
+  std::lock_guard<std::mutex> lk(g_web_aux_mu);
+  const WebAux *a = nullptr;
+  for (const WebAux &x : g_web_aux)
+    if (x.dev == dev && x.caller == caller) a = &x;
+  if (!a) {
+    WebAux x;
+    x.dev = dev;
+    x.caller = caller;
     for (int e = 0; e < 3; ++e)
-      if (hipEventCreateWithFlags(&evs[dev][e], hipEventDisableTiming) != hipSuccess)
-        return SG_ERR_HIP;
-    if (hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess)
-      return SG_ERR_HIP;
+      if (hipEventCreateWithFlags(&x.ev[e], hipEventDisableTiming) != hipSuccess) return SG_ERR_HIP;
+    if (hipStreamCreateWithFlags(&x.aux, hipStreamNonBlocking) != hipSuccess) return SG_ERR_HIP;
+    g_web_aux.push_back(x);
+    a = &g_web_aux.back();
   }
-  *gs = streams[dev];
-  *evF = evs[dev][0];
-  evG[0] = evs[dev][1];
-  evG[1] = evs[dev][2];
+  *gs = a->aux;
+  *evF = a->ev[0];
+  evG[0] = a->ev[1];
+  evG[1] = a->ev[2];
   return SG_OK;
+}
+
+int sg_web_release_aux() {
+  std::lock_guard<std::mutex> lk(g_web_aux_mu);
+  int rc = SG_OK;
+  int cur = 0;
+  const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+  for (WebAux &x : g_web_aux) {
+    if (hipSetDevice(x.dev) != hipSuccess) {
+      rc = SG_ERR_HIP;
+      continue;
+    }
+    // the second stream's work must be done before its objects go
+    if (hipStreamSynchronize(x.aux) != hipSuccess) rc = SG_ERR_HIP;
+    for (int e = 0; e < 3; ++e) (void)hipEventDestroy(x.ev[e]);
+    if (hipStreamDestroy(x.aux) != hipSuccess) rc = SG_ERR_HIP;
+  }
+  g_web_aux.clear();
+  if (have_cur) (void)hipSetDevice(cur);
+  return rc;
 }
 
 int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *pairs,
@@ -2437,7 +2473,7 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
   hipEvent_t evF = nullptr, evG[2] = {nullptr, nullptr};
   const int64_t nch = n_pairs > 0 ? (n_pairs + chunk - 1) / chunk : 0;
   if (pipe_env && nch > 1) {
-    if (web_aux(&gs, &evF, evG) != SG_OK) return SG_ERR_HIP;
+    if (web_aux(st, &gs, &evF, evG) != SG_OK) return SG_ERR_HIP;
   }
   const bool pipe = gs != st;
   struct Slot {

@@ -44,6 +44,7 @@ int sg_fast32_supported(const sg_model_t *m, const SgGenPlan &P);
 int sg_web_plan_params(const sg_model_t *m, int64_t *n_params);
 int sg_web_lds_ok(const sg_model_t *m);
 int64_t sg_web_ws_bytes(const sg_model_t *m, int64_t chunk, int64_t n_pairs);
+int sg_web_release_aux();
 int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *pairs,
                const float *labels, int64_t n_pairs, int64_t pair_offset, int64_t batch_total,
                const float *params, uint64_t seed, const float *y_stats, int add_label,
@@ -891,6 +892,8 @@ int64_t sg_web_workspace_bytes(const sg_model_t *model, int64_t chunk) {
   if (!model || chunk < 0) return -1;
   return sg_web_ws_bytes(model, chunk, -1);   // any n_pairs: both pipeline slots
 }
+
+int32_t sg_web_release(void) { return sg_web_release_aux(); }
 
 int64_t sg_web_workspace_bytes_ex(const sg_model_t *model, int64_t chunk, int64_t n_pairs) {
   if (!model || chunk < 0 || n_pairs < 0) return -1;

@@ -360,6 +360,11 @@ int64_t sg_web_workspace_bytes(const sg_model_t *model, int64_t chunk);
  * to n_pairs pairs. */
 int64_t sg_web_workspace_bytes_ex(const sg_model_t *model, int64_t chunk, int64_t n_pairs);
 
+/* Destroys the auxiliary streams and events of the sg_web_* chunk pipeline (one set per
+ * device and caller stream, created on first use), after waiting for their work: call at
+ * teardown, when no sg_web_* call is in flight (library 1.8).  Returns SG_OK or SG_ERR_HIP. */
+int32_t sg_web_release(void);
+
 /* Pre-activation scores of the pairs pair_idx [n_pairs][2] (store graph ids);
  * replaces sess.run([pred_sim_without_act()]) like sg_forward. */
 int32_t sg_web_forward(const sg_model_t *model, const sg_csr_store_t *store,

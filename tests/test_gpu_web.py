@@ -197,3 +197,25 @@ def test_web_empty_batch(gpu):
                             y_stats=batch.y_stats)
     model.fwd_bwd(empty, seed=1)
     assert float(model.grad.abs().max().item()) == 0.0
+
+
+def test_web_pipeline_streams_per_caller_stream_and_release(gpu):
+    """The chunk pipeline's second stream is per (device, caller stream): steps issued on two
+    torch streams give the one-stream bits, and sg_web_release (teardown) destroys the
+    auxiliary streams, after which a call re-creates them."""
+    import torch
+    from graphembedding_amd import _lib
+    prob = small_problem(n_graphs=24, n_pairs=500, seed=14, n_lo=20, n_hi=128, n_max=128,
+                         p_extra=0.05)
+    model, chunked = prob.make_gpu_web_model(device=gpu, chunk=97)
+    ref = model.pred_sim_without_act(chunked, seed=4).clone()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        s_side = model.pred_sim_without_act(chunked, seed=4)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    assert torch.equal(s_side, ref)
+    _lib.web_release()
+    assert torch.equal(model.pred_sim_without_act(chunked, seed=4), ref)
+    _lib.web_release()
