@@ -50,9 +50,10 @@ def parse():
     p.add_argument('--chunk', type=int, default=4_000_000,
                    help='C4: pairs per packed chunk when a shard does not fit HBM')
     p.add_argument('--source', choices=('auto', 'records', 'store'), default='auto',
-                   help='C4 streamed: the kernel gathers pairs from the graph store (auto) or '
-                        'packs records per chunk (records); store: also the resident '
-                        'C2/C3 shard (diagnostic, no records at all)')
+                   help='C4: the kernel gathers pairs from the graph store in launches of '
+                        '--store-chunk pairs (auto), or records are packed, resident when the '
+                        'shard fits --resident-gb, else per --chunk (records); store: also the '
+                        'resident C2/C3 shard (diagnostic, no records at all)')
     p.add_argument('--store-chunk', type=int, default=25_000_000,
                    help='C4 streamed from the store: pairs per launch')
     p.add_argument('--resident-gb', type=float, default=150.0,
@@ -235,6 +236,12 @@ def main():
         a, b = shard_range(len(gs.graphs) ** 2, srank, sworld)
         from graphembedding_amd.packer import record_words
         streamed = (b - a) * 4 * record_words(gs.n_max, args.records) > args.resident_gb * 1e9
+        # the capacity-32 kernel gathers pairs from the cache-resident dense store faster than
+        # it reads 8.5 KB records from HBM (an emulated W = 8 rank's resident shard: 148.9
+        # against 134.3 M pairs/s, profiles/r04_c4s/), so its shards are store-sourced
+        # whatever their size (--source records packs and keeps records)
+        if args.source == 'auto' and model.kernel_path == 2 and args.records == 'f32':
+            streamed = True
     if streamed:
         store_src = args.source == 'auto' and model.kernel_path == 2 and args.records == 'f32'
         shard = AllPairsStream(gs, labels, srank, sworld, device=device,
@@ -404,7 +411,8 @@ def main():
             elif streamed:
                 inputs = 'packed in chunks of {} pairs inside the step'.format(shard.chunk)
             else:
-                inputs = 'records resident in HBM'
+                inputs = ('graph store resident in HBM; the kernel gathers each pair\'s graphs '
+                          '(no records)' if args.source == 'store' else 'records resident in HBM')
             records = '{} Â, {} B/pair'.format(args.records, bytes_pair)
         out = {
             # BASELINE.json's metric string for the headline config (C2); the other
