@@ -153,7 +153,8 @@ class AllPairsStream(object):
 
     def __init__(self, gs: GraphSet, labels: np.ndarray, rank: int = 0, world: int = 1,
                  device='cuda', chunk: int = 4_000_000, dtype: str = 'f32',
-                 n_pairs: Optional[int] = None, balance: bool = True, source: str = 'auto'):
+                 n_pairs: Optional[int] = None, balance: bool = True, source: str = 'auto',
+                 keep_orders: bool = True):
         import torch
         self.torch = torch
         G = len(gs.graphs)
@@ -179,6 +180,11 @@ class AllPairsStream(object):
         self.source = source
         self.records = None   # allocated on the first packed chunk
         self.status = torch.zeros(1, dtype=torch.int32, device=device)
+        # store-sourced chunks need no records, so their batches (with the class order, 4 B
+        # per pair) are built once and reused by every step, as AllPairsShard reuses its
+        # packed, ordered batch; keep_orders=False rebuilds them per step
+        self.keep_orders = keep_orders
+        self._batches = {}
 
     def chunks(self):
         for c0 in range(self.start, self.end, self.chunk):
@@ -193,10 +199,16 @@ class AllPairsStream(object):
         model.check_node_counts(self.store.n, 'AllPairsStream')
         lab = self.labels[c0 - self.start:c0 - self.start + n]
         if self.uses_store(model):
+            key = (id(model), c0, n)
+            if self.keep_orders and key in self._batches:
+                return self._batches[key]
             b = model.batch_from_store(self.store, n, lab, grid_base=c0, pair_offset=c0,
                                        batch_total=self.total, y_stats=self.y_stats,
                                        status=self.status)
-            return model.balance(b) if self.balance else b
+            b = model.balance(b) if self.balance else b
+            if self.keep_orders:
+                self._batches[key] = b
+            return b
         if self.records is None:
             self.records = torch.empty(self.chunk * record_words(self.store.n_max, self.dtype),
                                        dtype=torch.int32, device=self.device)
@@ -206,6 +218,15 @@ class AllPairsStream(object):
         b = model.batch_from_records(self.records, n, lab, pair_offset=c0,
                                      batch_total=self.total, y_stats=self.y_stats)
         return model.balance(b) if self.balance else b
+
+    def prepare(self, model):
+        """Build (and keep) every store-sourced chunk's batch and class order before the
+        timed steps; returns the number of chunks prepared."""
+        if not (self.keep_orders and self.uses_store(model)):
+            return 0
+        for c0, n in self.chunks():
+            self._pack(model, c0, n)
+        return len(self._batches)
 
     def fwd_bwd(self, model, add_label_term: bool = True):
         """One fwd+bwd over the shard; leaves the summed gradient / loss_mse in
