@@ -107,3 +107,21 @@ def test_workspace_one_slot_for_single_chunk_calls():
     assert one == _lib.web_workspace_bytes(m, 4096, 0) and one < two
     # the slots dominate: the second one is most of the difference from the per-call part
     assert two - one > 0.4 * two
+
+
+def test_model_web_workspace_slots():
+    """model.web_workspace: a batch that fits one chunk gets the one-slot size, a longer one
+    both slots; a two-slot workspace already allocated serves one-chunk calls too."""
+    from graphembedding_amd.model_mse import SiameseGCNTNMSE
+    prob = small_problem(n_graphs=6, n_pairs=6, n_lo=20, n_hi=60, n_max=64)
+    m = SiameseGCNTNMSE(prob.d_in, prob.flags, device='cpu', n_max=64)
+    assert m.is_web
+    one = _lib.web_workspace_bytes(m.sg, 512, 512)
+    two = _lib.web_workspace_bytes(m.sg, 512)
+    w1 = m.web_workspace(512, 100)
+    assert w1.numel() * 4 >= one and w1.numel() * 4 < two
+    w2 = m.web_workspace(512, 5000)               # several chunks: grows to both slots
+    assert w2.numel() * 4 >= two
+    assert m.web_workspace(512, 10).data_ptr() == w2.data_ptr()   # reused
+    w3 = m.web_workspace(256, 10)                 # another chunk size: reallocated
+    assert w3.numel() * 4 >= _lib.web_workspace_bytes(m.sg, 256, 10)
