@@ -145,3 +145,32 @@ def test_fast32_store_source_matches_records(gpu):
     model.fwd_bwd(b_bad, seed=seed)
     torch.cuda.synchronize()
     assert int(status.item()) == _lib.SG_ERR_ARG
+
+
+def test_fast32_grid_past_its_end(gpu):
+    """A grid launch that runs past G² (the kernel's 64-bit id split instead of the 32-bit
+    multiply-high one): the pairs inside the grid score as the same pairs given by list,
+    and the ones past it raise the status word."""
+    import torch
+    from graphembedding_amd import _lib
+    from graphembedding_amd.packer import GraphStore
+    prob = small_problem(n_graphs=30, n_pairs=8, seed=41, n_lo=1, n_hi=30, n_max=30)
+    model, _ = prob.make_gpu_model(device=gpu)
+    assert model.kernel_path == 2
+    G = 30
+    store = GraphStore(prob.mgs, model.n_max, prob.d_in)
+    base, n_in, n = G * G - 5, 5, 20
+    q = np.arange(base, base + n_in)
+    pairs = torch.from_numpy(np.stack([q // G, q % G], axis=1).astype(np.int32)).to(gpu)
+    lab = torch.from_numpy(np.random.default_rng(5).random(n).astype(np.float32)).to(gpu)
+    status = torch.zeros(1, dtype=torch.int32, device=gpu)
+    b_list = model.batch_from_store(store, n_in, lab[:n_in], pair_idx=pairs, pair_offset=base,
+                                    status=status)
+    s_list = model.pred_sim_without_act(b_list, seed=3).clone()
+    torch.cuda.synchronize()
+    assert int(status.item()) == 0
+    b_over = model.batch_from_store(store, n, lab, grid_base=base, pair_offset=base, status=status)
+    s_over = model.pred_sim_without_act(b_over, seed=3).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(s_over[:n_in], s_list)
+    assert int(status.item()) == _lib.SG_ERR_ARG
