@@ -692,7 +692,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
               float *T = sT + s * 16 * TS1 + (4 * g + r) * TS1 + 16 * t + j;
               if (r < (s ? K1 : K0)) {
                 const uint32_t d = s ? (h >> 16) : (h & 0xFFFFu);
-                const float v = fmaxf(p1[s][t][r], 0.f);
+                const float v = relu_bits(p1[s][t][r]);
                 *T = d < A.thr1 ? v : 0.f;
               } else {
                 *T = 0.f;

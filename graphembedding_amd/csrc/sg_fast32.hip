@@ -91,6 +91,11 @@ struct F32Args {
   const uint4 *sadj, *stypes;   // [G][NC·NC/4], [G][NC/4] 16-B words
   const int32_t *sn, *spairs;   // [G], [n_pairs][2] or NULL (all-pairs grid)
   int64_t grid_base;
+  // all-pairs grid with G² < 2^32: q = grid_base + p splits as (q / G, q % G) by one
+  // 32-bit multiply-high with gm = ceil(2^32 / G) and one correction (scalar code) instead
+  // of the 64-bit division routine (≈130 SALU and two branches per pair)
+  uint32_t gm;
+  int g32;
   const float *slabels;
   int32_t *status;
 };
@@ -101,6 +106,14 @@ __device__ __forceinline__ bool f32_pair_ids(const F32Args &A, int p, int &g0, i
   if (A.spairs) {
     g0 = A.spairs[2 * (int64_t)p];
     g1 = A.spairs[2 * (int64_t)p + 1];
+  } else if (A.g32) {
+    // q < 2^32: gm = ceil(2^32 / G) overestimates q / G by less than q / 2^32 < 1, so the
+    // high product is q / G rounded down or one above it
+    const uint32_t q = (uint32_t)(A.grid_base + p), G = (uint32_t)A.G;
+    uint32_t d = __umulhi(q, A.gm);
+    d -= (d * G > q) ? 1u : 0u;
+    g0 = (int)d;
+    g1 = (int)(q - d * G);
   } else {
     const int64_t q = A.grid_base + p;
     g0 = (int)(q / A.G);
@@ -318,20 +331,24 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
         if (!ok && l == 0 && A.status) atomicExch(A.status, (int32_t)SG_ERR_ARG);
         const uint4 *a0 = A.sadj + (size_t)g0 * ADJ4, *a1 = A.sadj + (size_t)g1 * ADJ4;
         const uint4 *t0 = A.stypes + (size_t)g0 * (NC / 4), *t1 = A.stypes + (size_t)g1 * (NC / 4);
+        // the loads go out unconditionally (f32_pair_ids clamps invalid ids to graph 0);
+        // an invalid pair's words are zeroed afterwards, in one uniform branch
 #pragma unroll
         for (int c = 0; c < NREC; ++c) {
           const int w4 = l + 64 * c;
           uint4 x = uint4{0u, 0u, 0u, 0u};
-          if (ok) {
-            if (w4 < ADJ4) x = a0[w4];
-            else if (w4 < 2 * ADJ4) x = a1[w4 - ADJ4];
-            else if (w4 < 2 * ADJ4 + NC / 4) x = t0[w4 - 2 * ADJ4];
-            else if (w4 < 2 * ADJ4 + NC / 2) x = t1[w4 - 2 * ADJ4 - NC / 4];
-            else if (w4 == 2 * ADJ4 + NC / 2)
-              x = uint4{(uint32_t)A.sn[g0], (uint32_t)A.sn[g1],
-                        __float_as_uint(A.slabels ? A.slabels[p] : 0.f), (uint32_t)p};
-          }
+          if (w4 < ADJ4) x = a0[w4];
+          else if (w4 < 2 * ADJ4) x = a1[w4 - ADJ4];
+          else if (w4 < 2 * ADJ4 + NC / 4) x = t0[w4 - 2 * ADJ4];
+          else if (w4 < 2 * ADJ4 + NC / 2) x = t1[w4 - 2 * ADJ4 - NC / 4];
+          else if (w4 == 2 * ADJ4 + NC / 2)
+            x = uint4{(uint32_t)A.sn[g0], (uint32_t)A.sn[g1],
+                      __float_as_uint(A.slabels ? A.slabels[p] : 0.f), (uint32_t)p};
           v[c] = x;
+        }
+        if (__builtin_expect(!ok, 0)) {
+#pragma unroll
+          for (int c = 0; c < NREC; ++c) v[c] = uint4{0u, 0u, 0u, 0u};
         }
       } else {
         const uint4 *src = (const uint4 *)(A.recs + (size_t)(uint32_t)p * (size_t)rw4h * 16u);
@@ -550,7 +567,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
   #pragma unroll
               for (int s = 0; s < 2; ++s) {
                 const uint32_t dr = s ? (h >> 16) : (h & 0xFFFFu);
-                const float v = fmaxf(d1[s][to][f][r], 0.f);
+                const float v = relu_bits(d1[s][to][f][r]);
                 d1[s][to][f][r] = (nb < (s ? KB1 : KB0) && dr < A.thr1) ? v : 0.f;
               }
             } else {
@@ -1106,6 +1123,12 @@ int sg_fast32_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void 
   A.sn = src ? src->n : nullptr;
   A.spairs = src ? src->pair_idx : nullptr;
   A.grid_base = src ? src->grid_base : 0;
+  {
+    const uint64_t G = src ? (uint64_t)(src->n_graphs > 0 ? src->n_graphs : 1) : 1u;
+    A.g32 = (src && src->pair_idx == nullptr && G * G <= 0xFFFFFFFFull &&
+             src->grid_base >= 0 && (uint64_t)src->grid_base + (uint64_t)n_pairs <= G * G) ? 1 : 0;
+    A.gm = (uint32_t)(((1ull << 32) + G - 1) / G);   // ceil(2^32 / G) (G >= 2: fits 32 bits)
+  }
   A.slabels = src ? src->labels : nullptr;
   A.status = src ? src->status : nullptr;
   if (src && (P.adj_dtype != SG_DTYPE_F32 || src->n_max != NC || src->n_graphs <= 0 ||

@@ -82,6 +82,14 @@ __device__ __forceinline__ f4 mfbf16(uint2 a, uint2 b, f4 c) {
                                                     __builtin_bit_cast(s4, b), c, 0, 0, 0);
 }
 
+// relu(x) = max(x, 0) as one v_max_i32 on the bits (an f32 with the sign bit set is a
+// negative int32, +0 and positive floats order as their bit patterns): fmaxf(x, 0)
+// compiles to two v_max_f32 in the kernels' IEEE mode (the first quiets a signalling
+// NaN), and LLVM folds v_med3_f32(x, 0, inf) back into that.  -0 maps to +0.
+__device__ __forceinline__ float relu_bits(float x) {
+  return __int_as_float(max(__float_as_int(x), 0));
+}
+
 // DPP lane move with bound_ctrl (no "old" operand to materialise), so the
 // compiler can fold it into the consuming VALU op (v_add_f32_dpp).
 template <int CTRL>
