@@ -68,6 +68,14 @@ constexpr int W1TS = 36; // W1ᵀ table row stride (32 + pad)
 #ifndef SG_FAST_MAXW
 #define SG_FAST_MAXW 8
 #endif
+// gD1 = gZ1·W1ᵀ takes gZ1 with nodes on the lanes' rows (its A operand): SG_GZ1T_LDS = 1
+// writes the gZ1 tile (nodes on the accumulator rows, as Âᵀ·gH2 leaves it) to the wave's
+// LDS and reads it back transposed; 0 computes that orientation a second time on the f32
+// MFMA (gH2ᵀ·Â, 2-3 MFMAs per side, 4 for a shared tile).  The values are bitwise the
+// same (Â is symmetric and both products sum over the same nodes in the same order).
+#ifndef SG_GZ1T_LDS
+#define SG_GZ1T_LDS 1
+#endif
 // waves per block: 8 = 2 waves per SIMD at up to 256 VGPRs per lane
 constexpr int MAXW = SG_FAST_MAXW;
 
@@ -175,7 +183,10 @@ struct FastLds {
   static constexpr int GE = X + 48;                   // AVG: ∂L/∂x1 | ∂L/∂x2 (16 each)
   static constexpr int TMP = GE + 32;                 // ATT: node means of H2 (16 per side)
   static constexpr int GU = TMP + 32;                 // ATT: ∂L/∂(tanh input) (16 per side)
-  static int wave_floats(int) { return X + 48 + (AVG ? 32 : 0) + (ATT ? 64 : 0); }
+  static constexpr int GT = GU + 32;                  // SG_GZ1T_LDS: gZ1 tiles, 2 x 16 x TS2
+  static int wave_floats(int) {
+    return SG_GZ1T_LDS ? GT + 2 * 16 * TS2 : X + 48 + (AVG ? 32 : 0) + (ATT ? 64 : 0);
+  }
   static int shared_floats(int d_in) {
     return (d_in + 1) * FH1 + 2 * DN * FK * WR + FK * VS + FH1 * W1S + FH2 * W1TS +
            (SG_GD1_BF16 ? 2 * 3 * 64 * 4 : 0) + (ATT ? FH2 * WAS : 0);
@@ -1086,14 +1097,27 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #pragma unroll
         for (int q = 0; q < KS; ++q) {
           gz1 = mfma4(af[s][q], gh2[s][q], gz1);
-          if (!PACK) gz1t[s] = mfma4(gh2[s][q], af[s][q], gz1t[s]);
+          if (!PACK && !SG_GZ1T_LDS) gz1t[s] = mfma4(gh2[s][q], af[s][q], gz1t[s]);
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int q = 0; q < KS; ++q) gw1[t] = mfma4(dq[s][t][q], gz1[q], gw1[t]);
         SG_CLUSTER();
+#if SG_GZ1T_LDS
+        {   // gZ1 rows 4g + r, feature j (a shared tile: side 1's rows 2 below side 0's)
+          float *gt = W + L::GT + (PACK ? 0 : s * 16 * TS2) + j;
+#pragma unroll
+          for (int r = 0; r < KS; ++r) gt[(4 * g + r + ((PACK && s) ? 2 : 0)) * TS2] = gz1[r];
+        }
+#endif
       }
+#if SG_GZ1T_LDS
+      sg_wsync();
+#pragma unroll
+      for (int s = 0; s < (PACK ? 1 : 2); ++s)
+        gz1t[s] = *(const f4 *)(W + L::GT + s * 16 * TS2 + j * TS2 + 4 * g);
+#else
       if constexpr (PACK) {
         // gZ1ᵀ of both sides in the shared layout: side 0's Â rows are zero on the
         // lanes of side 1's rows (nodes >= 8 are absent), afp holds side 1's rows there
@@ -1107,6 +1131,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         gz1t[0] = c;
         SG_CLUSTER();
       }
+#endif
       // gD1 · ik1 = gZ1 (W1 ik1)ᵀ per feature tile t (one chain per tile when packed)
       f4 gd[2][2];   // [side, or 0 = shared][t]
 #if SG_GD1_BF16

@@ -64,6 +64,15 @@ constexpr int MAXW = 8;    // waves per block (2 per SIMD)
 #ifndef SG32_V_HOIST
 #define SG32_V_HOIST 0
 #endif
+// gD1 = gZ1·W1ᵀ takes gZ1 with nodes on the lanes' rows (its A operand): SG32_GZ1T_LDS = 1
+// writes the gZ1 tiles (nodes on the accumulator rows) to the wave's D1 tile, free in the
+// backward, and reads them back transposed; 0 computes that orientation a second time on
+// the f32 MFMA (gH2ᵀ·Â: one MFMA per live k-block and tile).  Bitwise the same values.
+// Measured on C4 (profiles/r04_gz1t/c4): 152.1 / 152.3 against 152.3 / 152.2 M pairs/s
+// (the spills grow by 4 VGPRs), so the MFMA form stays the default here; sg_fast gains.
+#ifndef SG32_GZ1T_LDS
+#define SG32_GZ1T_LDS 0
+#endif
 
 
 struct F32Args {
@@ -847,7 +856,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
             for (int b = 0; b < 8; ++b) {
               if (kb_live(b, T, KB)) {
                 gz1[to] = mfma4(af[to][b], gh2[b >> 2][b & 3], gz1[to]);
-                gz1t[to] = mfma4(gh2[b >> 2][b & 3], af[to][b], gz1t[to]);
+                if (!SG32_GZ1T_LDS) gz1t[to] = mfma4(gh2[b >> 2][b & 3], af[to][b], gz1t[to]);
               }
             }
           }
@@ -860,6 +869,19 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
             for (int f = 0; f < 2; ++f) gw1[f] = mfma4(d1[s][b >> 2][f][b & 3], gz1[b >> 2][b & 3], gw1[f]);
           }
         }
+  #if SG32_GZ1T_LDS
+        // gZ1 rows 16 to + 4g + r, feature j into the tile; read back as row 16 to + j,
+        // features 4g..4g+3 (the previous side's reads are done: program order)
+  #pragma unroll
+        for (int to = 0; to < 2; ++to)
+          if (to < T)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) sT[(16 * to + 4 * g + r) * TS1 + j] = gz1[to][r];
+        sg_wsync();
+  #pragma unroll
+        for (int to = 0; to < 2; ++to)
+          if (to < T) gz1t[to] = *(const f4 *)(sT + (16 * to + j) * TS1 + 4 * g);
+  #endif
         // gD1 · ik1 = gZ1 (W1 ik1)ᵀ; gP1 = keep·relu' (D1 > 0); gZ0 = Âᵀ gP1
         f4 gp1[2][2];   // [to][f]
   #pragma unroll

@@ -805,7 +805,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
             const int f = 16 * c + 4 * g + s;
-            const float hv = h[4 * c + s] > 0.f ? h[4 * c + s] : 0.f;
+            const float hv = sgk::relu_bits(h[4 * c + s]);
             const bool k1 = use_mw ? ((mw[u] >> (4 * c + s)) & 1u) != 0u
                                    : web_fkeep(pk, 1, side, (uint32_t)(n * WH1 + f), A.thr1);
             if (!BWD) mw[u] |= (k1 ? 1u : 0u) << (4 * c + s);
@@ -871,7 +871,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
         part = fmaf(k2[s] ? h2[s] : 0.f, sWd[4 * g + s], part);
       }
       const float pre = sgk::xsum32(sgk::xsum16(part)) + bd;
-      const float z = pre > 0.f ? pre : 0.f;
+      const float z = sgk::relu_bits(pre);
       const bool k4 = n < N && (use_mw ? ((mw[u] >> 12) & 1u) != 0u
                                        : web_fkeep(pk, 4, side, (uint32_t)n, A.thr4));
       if (!BWD) {
