@@ -555,16 +555,18 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #define SG_PRIO_YOUNG 2
 #endif
   int it = 0;
-  const bool young = wv >= 4;
+  const int young = wv >> 2;   // 0 / 1, wave-uniform (scalar)
   // The pair loop: CLS < 0 = mixed schedule (each pair dispatches to its (K0, K1) body);
   // CLS = c: every pair of this wave has class c, one body, so the loop-carried
   // accumulators need no copies at a join of four bodies (≈55 v_mov_b32 per pair)
   auto pair_loop = [&](auto CLSc) __attribute__((always_inline)) {
   constexpr int CLS = decltype(CLSc)::value;
   for (; q < qend; ++it) {
-    const bool yturn = (it % SG_PRIO_PERIOD) < SG_PRIO_YOUNG;
-    if (yturn == young) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
+    // (scalar integers: as bools the comparison went through VALU selects; one
+    // conditional instead of an if / else)
+    const int yturn = (int)((unsigned)((it % SG_PRIO_PERIOD) - SG_PRIO_YOUNG) >> 31);   // < YOUNG
+    __builtin_amdgcn_s_setprio(0);
+    if ((yturn ^ young) == 0) __builtin_amdgcn_s_setprio(1);
     sg_wsync();
     if (A.rec_bf16) {
 #pragma unroll
