@@ -184,8 +184,10 @@ struct FastLds {
   static constexpr int TMP = GE + 32;                 // ATT: node means of H2 (16 per side)
   static constexpr int GU = TMP + 32;                 // ATT: ∂L/∂(tanh input) (16 per side)
   static constexpr int GT = GU + 32;                  // SG_GZ1T_LDS: gZ1 tiles, 2 x 16 x TS2
-  static int wave_floats(int) {
-    return SG_GZ1T_LDS ? GT + 2 * 16 * TS2 : X + 48 + (AVG ? 32 : 0) + (ATT ? 64 : 0);
+  // (the gZ1 tiles only in the backward: the forward-only kernel keeps its smaller
+  // regions and with them two blocks per CU)
+  static int wave_floats(int, bool bwd) {
+    return (SG_GZ1T_LDS && bwd) ? GT + 2 * 16 * TS2 : X + 48 + (AVG ? 32 : 0) + (ATT ? 64 : 0);
   }
   static int shared_floats(int d_in) {
     return (d_in + 1) * FH1 + 2 * DN * FK * WR + FK * VS + FH1 * W1S + FH2 * W1TS +
@@ -1340,7 +1342,7 @@ FastCfg fast_cfg_t(int d_in, int n_params, int64_t n_pairs, bool bwd) {
   using LL = FastLds<D, AVG, ATT>;
   using FS = FlushSlots<D, AVG, ATT>;
   c.shared_floats = LL::shared_floats(d_in);
-  c.wave_floats = LL::wave_floats(d_in);
+  c.wave_floats = LL::wave_floats(d_in, bwd);
   // resident waves per CU allowed by registers: the backward kernel uses up to
   // 256 VGPRs (2 waves / SIMD), the forward-only one ~120 (4 waves / SIMD)
   const int wcap = bwd ? MAXW : 2 * MAXW;
