@@ -12,6 +12,8 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import List, Optional
 
+import weakref
+
 import numpy as np
 
 from .data import synthetic_ged_matrix, synthetic_graphs
@@ -185,6 +187,7 @@ class AllPairsStream(object):
         # packed, ordered batch; keep_orders=False rebuilds them per step
         self.keep_orders = keep_orders
         self._batches = {}
+        self._batches_owner = None
 
     def chunks(self):
         for c0 in range(self.start, self.end, self.chunk):
@@ -199,7 +202,13 @@ class AllPairsStream(object):
         model.check_node_counts(self.store.n, 'AllPairsStream')
         lab = self.labels[c0 - self.start:c0 - self.start + n]
         if self.uses_store(model):
-            key = (id(model), c0, n)
+            # the kept batches belong to one model (a weak reference: a later model that
+            # reuses a dead one's id() must not get its batches)
+            owner = self._batches_owner() if self._batches_owner is not None else None
+            if owner is not model:
+                self._batches = {}
+                self._batches_owner = weakref.ref(model)
+            key = (c0, n)
             if self.keep_orders and key in self._batches:
                 return self._batches[key]
             b = model.batch_from_store(self.store, n, lab, grid_base=c0, pair_offset=c0,

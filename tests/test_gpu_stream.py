@@ -64,3 +64,36 @@ def test_stream_from_store_equals_resident_records(gpu, world, rank):
     g = model.grad_loss.cpu().numpy()
     scale = max(1.0, float(np.abs(g_ref).max()))
     assert float(np.abs(g - g_ref).max()) <= 1e-5 * scale
+
+
+def test_stream_kept_batches_are_per_model(gpu):
+    """Store-sourced chunk batches are built once (prepare) and reused by later steps of the
+    same model; a second model gets batches of its own, and a step over the kept batches
+    equals one that rebuilds them (keep_orders=False)."""
+    from graphembedding_amd.allpairs import AllPairsStream, load_graph_set
+    from graphembedding_amd.config import Flags
+    from graphembedding_amd.model_mse import SiameseGCNTNMSE
+    flags = Flags(dropout=0.1, **C4_FLAGS)
+    gs = load_graph_set('syn_aids80nef', n_max=32)
+    labels = gs.label_matrix(flags.yeta)
+    m1 = SiameseGCNTNMSE(gs.d_in, flags, device=gpu, n_max=gs.n_max)
+    m2 = SiameseGCNTNMSE(gs.d_in, flags, device=gpu, n_max=gs.n_max)
+    kept = AllPairsStream(gs, labels, 0, 1, device=gpu, chunk=1111, balance=True)
+    fresh = AllPairsStream(gs, labels, 0, 1, device=gpu, chunk=1111, balance=True,
+                           keep_orders=False)
+    n_chunks = len(list(kept.chunks()))
+    assert kept.prepare(m1) == n_chunks > 1
+    b1 = kept._pack(m1, kept.start, min(kept.chunk, kept.end - kept.start))
+    assert kept._pack(m1, kept.start, min(kept.chunk, kept.end - kept.start)) is b1
+    b2 = kept._pack(m2, kept.start, min(kept.chunk, kept.end - kept.start))
+    assert b2 is not b1
+    seed = 7
+    grads = []
+    for st in (kept, fresh):
+        orig = m2.fwd_bwd
+        m2.fwd_bwd = lambda b, add_label_term=True: orig(b, seed=seed,
+                                                          add_label_term=add_label_term)
+        st.fwd_bwd(m2)
+        m2.fwd_bwd = orig
+        grads.append(m2.grad_loss.cpu().numpy().copy())
+    assert np.array_equal(grads[0], grads[1])
