@@ -540,6 +540,11 @@ __host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, int max_nnz, bool b
 #ifndef SG_WEB_ROWP
 #define SG_WEB_ROWP 0
 #endif
+// the CSR row extents of a lane's rows loaded once per unit (1) or before each row's
+// gather (0)
+#ifndef SG_WEB_ROW_EXT
+#define SG_WEB_ROW_EXT 1
+#endif
 template <typename CT, typename F>
 __device__ __forceinline__ void csr_row(const CT *__restrict__ col, const float *__restrict__ val,
                                         int e0, int e1, F f) {
@@ -775,6 +780,23 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
     const int gszn = un_.y;
     const int4 inn = qn >= 0 ? ginst[qn] : make_int4(0, 0, 0, 0);
     __syncthreads();
+    // the CSR extents of this lane's rows (node 16t + i of each of its tiles), loaded
+    // together once per unit: every one-row-per-lane phase below starts from them
+    // instead of a dependent row-pointer load before each row's gather
+    int re0[GCN_TPW], re1[GCN_TPW];
+#pragma unroll
+    for (int u = 0; u < GCN_TPW; ++u) {
+      const int n = 16 * (lw + u * WPI) + i;
+      const bool in_ = SG_WEB_ROW_EXT && n < N;
+      re0[u] = in_ ? rp[n] : 0;
+      re1[u] = in_ ? rp[n + 1] : 0;
+    }
+    auto row0 = [&](int u, int n) __attribute__((always_inline)) -> int {
+      return SG_WEB_ROW_EXT ? re0[u] : rp[n];
+    };
+    auto row1 = [&](int u, int n) __attribute__((always_inline)) -> int {
+      return SG_WEB_ROW_EXT ? re1[u] : rp[n + 1];
+    };
 
     // ---- forward: H1 (lane (i, g): node 16t+i, features 16c + 4g + s), D1', Z1 ----
 #pragma unroll
@@ -792,7 +814,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
 #ifdef SG_WEB_ABL_FH1   // timing ablation only (results invalid): the forward skips the H1 gather
         if (BWD)
 #endif
-        csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
+        csr_row(cl, vl, row0(u, n), row1(u, n), [&](int mm, float v) {
           const float *wr = sW0 + sEtk[mm] * W0S + 4 * g;
           const float4 wa = *(const float4 *)wr, wb = *(const float4 *)(wr + 16);
           h[0] = fmaf(v, wa.x, h[0]); h[1] = fmaf(v, wa.y, h[1]);
@@ -855,7 +877,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
 #ifdef SG_WEB_ABL_FH2   // timing ablation only (results invalid): the forward skips the H2 gather
         if (BWD)
 #endif
-        csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
+        csr_row(cl, vl, row0(u, n), row1(u, n), [&](int mm, float v) {
           const float4 zz = *(const float4 *)(sZ1k + mm * ZS + 4 * g);
           h2[0] = fmaf(v, zz.x, h2[0]); h2[1] = fmaf(v, zz.y, h2[1]);
           h2[2] = fmaf(v, zz.z, h2[2]); h2[3] = fmaf(v, zz.w, h2[3]);
@@ -925,7 +947,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
       const int n = 16 * t + i;
       float q4[4] = {0.f, 0.f, 0.f, 0.f};
       if (n < N)
-        csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
+        csr_row(cl, vl, row0(u, n), row1(u, n), [&](int mm, float v) {
           const float4 gg = *(const float4 *)(sZ1k + mm * ZS + 4 * g);
           q4[0] = fmaf(v, gg.x, q4[0]); q4[1] = fmaf(v, gg.y, q4[1]);
           q4[2] = fmaf(v, gg.z, q4[2]); q4[3] = fmaf(v, gg.w, q4[3]);
@@ -988,7 +1010,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
       {
         const int n = 16 * t + i;
         if (n < N && sEtk[n] < d_in)
-          csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
+          csr_row(cl, vl, row0(u, n), row1(u, n), [&](int mm, float v) {
             const float *dr = sD1k + mm * DS + 4 * g;
             const float4 da = *(const float4 *)dr, db = *(const float4 *)(dr + 16);
             hq[0] = fmaf(v, da.x, hq[0]); hq[1] = fmaf(v, da.y, hq[1]);
