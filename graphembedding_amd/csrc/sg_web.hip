@@ -545,6 +545,10 @@ __host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, int max_nnz, bool b
 #ifndef SG_WEB_ROW_EXT
 #define SG_WEB_ROW_EXT 1
 #endif
+// csr_row's tail of fewer than four entries: a pair, then a single (1), or one at a time (0)
+#ifndef SG_WEB_TAIL2
+#define SG_WEB_TAIL2 1
+#endif
 template <typename CT, typename F>
 __device__ __forceinline__ void csr_row(const CT *__restrict__ col, const float *__restrict__ val,
                                         int e0, int e1, F f) {
@@ -574,7 +578,19 @@ __device__ __forceinline__ void csr_row(const CT *__restrict__ col, const float 
     f(c2, v2);
     f(c3, v3);
   }
+#if SG_WEB_TAIL2
+  // a tail of 2-3 entries as a pair then a single (two dependent round trips, not three)
+  if (e + 2 <= e1) {
+    const int c0 = col[e], c1 = col[e + 1];
+    const float v0 = val[e], v1 = val[e + 1];
+    f(c0, v0);
+    f(c1, v1);
+    e += 2;
+  }
+  if (e < e1) f(col[e], val[e]);
+#else
   for (; e < e1; ++e) f(col[e], val[e]);
+#endif
 #endif
 }
 
