@@ -304,14 +304,14 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
 #ifndef SG_PRIO32_YOUNG
 #define SG_PRIO32_YOUNG 2
 #endif
-  const bool young = wv >= 4;
+  const int young = wv >> 2;   // 0 / 1, wave-uniform (scalar)
   for (int it = 0;; ++it) {
     const int q = slot_of(it);
     if (q >= npairs) break;
     if (SG_PRIO32_PERIOD > 0) {
-      const bool yturn = (it % SG_PRIO32_PERIOD) < SG_PRIO32_YOUNG;
-      if (yturn == young) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
+      const int yturn = (int)((unsigned)((it % SG_PRIO32_PERIOD) - SG_PRIO32_YOUNG) >> 31);
+      __builtin_amdgcn_s_setprio(0);   // (scalar, one conditional, as sg_fast)
+      if ((yturn ^ young) == 0) __builtin_amdgcn_s_setprio(1);
     }
     const int p = pnext;
     // ---- stage the record (f32 LDS image; bf16 Â widened) ----
