@@ -68,9 +68,11 @@ def build_hip(force: bool = False, verbose: bool = False, out: str = None, defin
     variant = out is not None
     extra = os.environ.get('SG_EXTRA_FLAGS', '').split() if variant else []
     defines = tuple(defines) if variant else ()
-    if any(d.split('=')[0] == 'SG_TIMING_ABLATION_BUILD' for d in defines) and \
-            os.path.abspath(dst) == os.path.abspath(OUT):
-        raise RuntimeError('timing-ablation builds never go to the product library path')
+    # defines, SG_EXTRA_FLAGS (-D...) and SG_FLAGS_<SRC> can all carry timing-ablation or
+    # A/B macros: no variant build may write the product library path
+    if variant and os.path.abspath(dst) == os.path.abspath(OUT):
+        raise RuntimeError('A/B variant builds (out=...) never go to the product library '
+                           'path {}'.format(OUT))
     base += ['-D' + d for d in defines]
     base += extra
     per_source = {}

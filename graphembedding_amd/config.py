@@ -55,6 +55,10 @@ DEFAULTS: Dict[str, Any] = dict(
     ntn_mode='reference',      # 'reference' = (ΣU)·Σ relu(m) quirk (A1) | 'intended'
     label_stream='compat',     # 'compat' = labels from a later sampler draw (A3) | 'aligned'
     test_matrix='full',        # 'full' = sim_mat[i][j] | 'compat_diag' = sim_mat[i][i] (A5)
+    # one-hot type -> column map: 'set' = Python set iteration order as graphs.py:101-104
+    # (PYTHONHASHSEED-dependent for string types, quirk A7) | 'sorted' = sorted by str, the
+    # same in every process (tests, multi-rank runs)
+    node_feat_order='set',
     # test_time_mat: 'batched' = one launch for all m x n pairs, every entry the launch time
     # / (m n) (a deviation from the reference, recorded on the result); 'per_pair' = one
     # timed single-pair launch per entry, as train.py:57-69 times each sess.run

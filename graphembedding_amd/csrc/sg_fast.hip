@@ -245,8 +245,10 @@ __device__ __forceinline__ int fast_param(const FastArgs &A, int s, int l) {
   return (ATT && s < 4) ? A.oWa + (4 * s + g) * FH2 + j : -1;
 }
 
-// tanh and the logistic function from v_exp_f32 and v_rcp_f32 (≈1e-7 relative; the
-// Attention layer's h and att, layers.py:156-157)
+// tanh and the logistic function from v_exp_f32 and v_rcp_f32 (the Attention layer's h
+// and att, layers.py:156-157).  Both are ≈1e-7 ABSOLUTE error: sg_tanh's 1 - 2/(e^2z + 1)
+// cancels for small |z| (relative error ≈1e-7/|z|, e.g. 1e-3 at |z| = 1e-4), which the
+// oracle tolerances (1e-4 on the score) absorb
 __device__ __forceinline__ float sg_tanh(float z) {
   return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * z) + 1.f);
 }

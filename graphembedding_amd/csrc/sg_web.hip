@@ -2276,9 +2276,15 @@ int sg_web_plan_params(const sg_model_t *m, int64_t *n_params) {
 int64_t sg_web_ws_bytes(const sg_model_t *m, int64_t chunk, int64_t n_pairs) {
   WebPlan W;
   if (web_plan(m, &W) != SG_OK) return -1;
+  // chunk <= 0 is one chunk of the whole call, as sg_web_run reads it: sizable only for a
+  // known n_pairs
+  if (chunk <= 0) {
+    if (n_pairs < 0) return -1;
+    chunk = n_pairs > 0 ? n_pairs : 1;
+  }
   const WebWs ws = web_ws(W, chunk);
   // calls of at most one chunk never pipeline (sg_web_run): slot 0 only
-  const bool one = n_pairs >= 0 && n_pairs <= (chunk > 0 ? chunk : 1);
+  const bool one = n_pairs >= 0 && n_pairs <= chunk;
   return (one ? ws.total1 : ws.total) * 4 + 256;
 }
 
@@ -2376,32 +2382,56 @@ int sg_web_lds_ok(const sg_model_t *m) {
 // instance kernel done, G[slot] = the GEMMs of the chunk in that workspace slot done), one
 // set per (device, caller stream): calls on different caller streams do not share a second
 // stream (no false dependency between them), and calls from any host thread on the same
-// caller stream reuse one set.  sg_web_release() destroys them all (teardown).
+// caller stream reuse one set.  The registry is a small LRU (kWebAuxMax sets): a caller
+// that churns through short-lived streams recycles the least recently used set (after its
+// second stream drains) instead of growing the list.  A caller stream whose handle is
+// reused after it was destroyed inherits that set, which is harmless: the set only orders
+// the call's own work.  sg_web_release() destroys them all (teardown).
 struct WebAux {
   int dev;
   hipStream_t caller, aux;
   hipEvent_t ev[3];
+  uint64_t last_use;
 };
+constexpr size_t kWebAuxMax = 16;
 static std::mutex g_web_aux_mu;
 static std::vector<WebAux> g_web_aux;
+static uint64_t g_web_aux_tick = 0;
 
 static int web_aux(hipStream_t caller, hipStream_t *gs, hipEvent_t *evF, hipEvent_t *evG) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return SG_ERR_HIP;
   std::lock_guard<std::mutex> lk(g_web_aux_mu);
-  const WebAux *a = nullptr;
-  for (const WebAux &x : g_web_aux)
+  WebAux *a = nullptr;
+  for (WebAux &x : g_web_aux)
     if (x.dev == dev && x.caller == caller) a = &x;
   if (!a) {
     WebAux x;
     x.dev = dev;
     x.caller = caller;
-    for (int e = 0; e < 3; ++e)
-      if (hipEventCreateWithFlags(&x.ev[e], hipEventDisableTiming) != hipSuccess) return SG_ERR_HIP;
-    if (hipStreamCreateWithFlags(&x.aux, hipStreamNonBlocking) != hipSuccess) return SG_ERR_HIP;
-    g_web_aux.push_back(x);
-    a = &g_web_aux.back();
+    x.last_use = 0;
+    if (g_web_aux.size() >= kWebAuxMax) {
+      // recycle the least recently used set of this device (its queued work first)
+      WebAux *lru = nullptr;
+      for (WebAux &y : g_web_aux)
+        if (y.dev == dev && (!lru || y.last_use < lru->last_use)) lru = &y;
+      if (lru) {
+        if (hipStreamSynchronize(lru->aux) != hipSuccess) return SG_ERR_HIP;
+        lru->caller = caller;
+        a = lru;
+      }
+    }
+    if (!a) {
+      for (int e = 0; e < 3; ++e)
+        if (hipEventCreateWithFlags(&x.ev[e], hipEventDisableTiming) != hipSuccess)
+          return SG_ERR_HIP;
+      if (hipStreamCreateWithFlags(&x.aux, hipStreamNonBlocking) != hipSuccess)
+        return SG_ERR_HIP;
+      g_web_aux.push_back(x);
+      a = &g_web_aux.back();
+    }
   }
+  a->last_use = ++g_web_aux_tick;
   *gs = a->aux;
   *evF = a->ev[0];
   evG[0] = a->ev[1];

@@ -889,7 +889,7 @@ int32_t sg_adam_tf_ex(float *params, float *m, float *v, const float *grad, int6
 }
 
 int64_t sg_web_workspace_bytes(const sg_model_t *model, int64_t chunk) {
-  if (!model || chunk < 0) return -1;
+  if (!model || chunk <= 0) return -1;   // chunk 0 = n_pairs: use sg_web_workspace_bytes_ex
   return sg_web_ws_bytes(model, chunk, -1);   // any n_pairs: both pipeline slots
 }
 

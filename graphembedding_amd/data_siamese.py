@@ -19,6 +19,7 @@ class SiameseModelData(object):
         self.sampler = f.sampler
         self.sample_num = f.sample_num
         self.sampler_duplicate_removal = f.sampler_duplicate_removal
+        self.node_feat_order = getattr(f, 'node_feat_order', 'set')
         self.init()
 
     def init(self):
@@ -80,7 +81,12 @@ class SiameseModelData(object):
 
     def _get_node_feature_encoder(self, gs):
         if self.node_feat_encoder == 'onehot':
-            return NodeFeatureOneHotEncoder(gs, self.node_feat_name)
+            enc = NodeFeatureOneHotEncoder(gs, self.node_feat_name)
+            if self.node_feat_order == 'sorted':
+                return enc.pin_sorted()
+            if self.node_feat_order != 'set':
+                raise RuntimeError('Unknown node_feat_order {}'.format(self.node_feat_order))
+            return enc
         raise RuntimeError('Unknown node_feat_encoder {}'.format(self.node_feat_encoder))
 
     def _get_graph_collection(self, train_val_test):

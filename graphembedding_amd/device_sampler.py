@@ -18,21 +18,19 @@ Nothing crosses PCIe per step.
 """
 from __future__ import annotations
 
-import random
 from typing import Optional
 
 import numpy as np
 
 from . import _lib
+from . import samplers
 from .packer import GraphStore, pack_device_into, record_words
 from .samplers import DistributionSampler, RandomSampler
 
 
 def shuffle_permutation(n: int, seed: int = 123) -> np.ndarray:
     """σ with random.Random(seed).shuffle(x) == [x[σ[i]] for i in range(n)]."""
-    sigma = list(range(n))
-    random.Random(seed).shuffle(sigma)
-    return np.asarray(sigma, dtype=np.int32)
+    return np.asarray(samplers.shuffle_permutation(n, seed), dtype=np.int32)
 
 
 class DeviceRandomSampler(object):
@@ -84,8 +82,7 @@ class DeviceDistributionSampler(object):
         self.dens_order = torch.tensor([i for _, i in host.dens_list], dtype=torch.int32,
                                        device=device)
         self.bins = torch.tensor(host.bin_idx, dtype=torch.int32, device=device)
-        items = [random.Random(123 + c).randint(0, host.bin_size - 1)
-                 for c in range(0, n_bins, 2)]
+        items = [samplers.bin_item(c, host.bin_size) for c in range(0, n_bins, 2)]
         self.item_table = torch.tensor(items, dtype=torch.int32, device=device)
         self.state = torch.tensor([host.cur, host.item_idx], dtype=torch.int32, device=device)
         self.bin_size = host.bin_size

@@ -98,7 +98,8 @@ def test(data, dist_calculator, model, flags=None, evaluator=None, verbose=True)
                 s1 = model.test_scores(one)
                 _sync()
                 time_mat[i][j] = (_time.time() - t) * 1000.0
-                if s1[0] != s[i * n + j]:   # same keys, same kernel: bit-identical
+                # same keys, same kernel: bit-identical (bit patterns, so NaN == NaN)
+                if np.float64(s1[0]).view(np.uint64) != np.float64(s[i * n + j]).view(np.uint64):
                     raise RuntimeError('per_pair score ({}, {}) = {!r} differs from the batched '
                                        'score {!r}'.format(i, j, float(s1[0]),
                                                            float(s[i * n + j])))
@@ -123,8 +124,9 @@ def test(data, dist_calculator, model, flags=None, evaluator=None, verbose=True)
     return sim_mat, time_mat, results
 
 
-def main(flags=None, device='cuda'):
-    """main.py:14-27 (returns costs/times and the test results)."""
+def main(flags=None, device='cuda', return_objects=False):
+    """main.py:14-27 (returns costs/times and the test results; with return_objects also
+    the (data, dist_calculator, model) the run trained and scored with)."""
     from .data import synthetic_ged_matrix
     from .data_siamese import SiameseModelData
     from .dist_calculator import DistCalculator
@@ -146,6 +148,8 @@ def main(flags=None, device='cuda'):
     tr = train_val(data, dc, model, f)
     evaluator = Eval.from_calculator(data, dc, f) if f.dataset.startswith('syn_') else None
     res = test(data, dc, model, f, evaluator)
+    if return_objects:
+        return tr, res, (data, dc, model)
     return tr, res
 
 

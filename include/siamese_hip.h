@@ -349,11 +349,12 @@ typedef struct sg_csr_store {
 } sg_csr_store_t;
 
 /* Workspace bytes for sg_web_forward / sg_web_fwd_bwd processing chunks of up
- * to `chunk` pairs (any n_pairs is processed chunk by chunk). */
+ * to `chunk` pairs (any n_pairs is processed chunk by chunk).  chunk must be >= 1: a call
+ * with chunk <= 0 runs one chunk of n_pairs, sized by sg_web_workspace_bytes_ex; -1 here. */
 int64_t sg_web_workspace_bytes(const sg_model_t *model, int64_t chunk);
 
 /* Workspace bytes for sg_web_forward / sg_web_fwd_bwd calls of at most n_pairs pairs in
- * chunks of `chunk` (library 1.8).  A call of several chunks pipelines them over two
+ * chunks of `chunk` (library 1.8; chunk 0 = one chunk of n_pairs, as the calls read it).  A call of several chunks pipelines them over two
  * workspace slots (the NTN inputs, dropout keep bits and D2 rows of one chunk each, which
  * grow with chunk x node capacity); when n_pairs <= chunk there is one chunk and one slot,
  * about half of sg_web_workspace_bytes.  A workspace sized for n_pairs serves calls of up

@@ -516,6 +516,30 @@ def adam_tf_step(params, grad, st: AdamState, lr=0.01, beta1=0.9, beta2=0.999, e
     return new
 
 
+def adam_tf_step_f32(params, grad_mse, st: AdamState, lr=0.01, beta1=0.9, beta2=0.999,
+                     eps=1e-8, weight_decay=0.0):
+    """The same update in float32 arithmetic, as the reference trains (TF fp32 variables,
+    models.py:28-36).  Restates TF 1.x's CPU ApplyAdam functor (training_ops.cc, the
+    non-Nesterov branch; TF is absent here, version per SURVEY §8(c)):
+      alpha = lr*sqrt(1-b2p)/(1-b1p); m += (g-m)*(1-b1); v += (g*g-v)*(1-b2);
+      var -= (m*alpha)/(sqrt(v)+eps)
+    with g = dL_mse/dvar + wd*var, the AddN of the MSE gradient and l2_loss's gradient
+    (models.py:69-74).  st.m / st.v are kept float32."""
+    f = np.float32
+    th = np.asarray(params, f)
+    g = np.asarray(grad_mse, f) + f(weight_decay) * th
+    b1p, b2p = f(st.beta1_power), f(st.beta2_power)
+    alpha = f(lr) * np.sqrt(f(1) - b2p) / (f(1) - b1p)
+    m = np.asarray(st.m, f)
+    v = np.asarray(st.v, f)
+    m = m + (g - m) * (f(1) - f(beta1))
+    v = v + (g * g - v) * (f(1) - f(beta2))
+    st.m, st.v = m, v
+    st.beta1_power = float(b1p * f(beta1))
+    st.beta2_power = float(b2p * f(beta2))
+    return th - (m * alpha) / (np.sqrt(v) + f(eps))
+
+
 # ----------------------------------------------------------------------------
 # Default layer stacks (config.py:44-66; tuning.py:74-93)
 # ----------------------------------------------------------------------------

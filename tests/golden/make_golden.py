@@ -11,6 +11,7 @@ Pinned here (reference modules imported read-only, PYTHONDONTWRITEBYTECODE):
   src/metrics.py              precision_at_ks, mean_reciprocal_rank, mean_squared_error
   src/utils.py                sorted_nicely, save (F6: the label-store pickle)
   src/data.py                 AIDS700nefData / AIDS80nefData gexf loaders (F6)
+  model/Siamese/samplers.py   list order after the default 20-iteration loop (F7)
 Not importable here: TF (absent), src/distance.py and src/results.py (need bs4
 via nx_to_gxl.py) — their logic is restated and tested against these fixtures
 where it feeds them.
@@ -258,9 +259,33 @@ def f6_loaders():
     print('F6 fixtures written to', fx)
 
 
+def f7_train_loop_lists():
+    """F7 (row f1, quirks A3 + A6): the reference RandomSampler's list order after a whole
+    default training loop.  train_val (train.py:8-44) makes, per iteration, one train and
+    one val get_feed_dict; each draws B + B² = 30 pairs (A3), so after `iters` iterations
+    both the 52-graph train list and the 18-graph val list of AIDS80nef
+    (data_siamese.py:85-87) have seen 30 * iters get_pair calls, each wrap shuffling the
+    list in place (samplers.py:28).  test() then scores column j against that permuted
+    list (data_siamese.py:58-66)."""
+    out = {}
+    for n in (52, 18):
+        for iters in (1, 4, 20):
+            s = ref_samplers.RandomSampler(list(range(n)), -1, False)
+            for _ in range(30 * iters):
+                s.get_pair()
+            out['random_{}_after_{}_calls'.format(n, 30 * iters)] = {'gs': list(s.gs),
+                                                                     'idx': int(s.idx)}
+    with open(os.path.join(HERE, 'f7_loop_lists.json'), 'w') as f:
+        json.dump(out, f)
+    print('F7 fixtures written to', HERE)
+
+
 if __name__ == '__main__':
     if '--only-f6' in sys.argv:
         f6_loaders()
+    elif '--only-f7' in sys.argv:
+        f7_train_loop_lists()
     else:
         main()
         f6_loaders()
+        f7_train_loop_lists()

@@ -18,7 +18,7 @@ def test_graph_steps_equal_eager_steps(gpu, stack):
     from graphembedding_amd.dist_calculator import DistCalculator
     from graphembedding_amd.model_mse import SiameseGCNTNMSE
     ov = dict(AVERAGE_STACK) if stack == 'average' else {}
-    f = Flags(dataset='syn_aids80nef', **ov)
+    f = Flags(dataset='syn_aids80nef', node_feat_order='sorted', **ov)
 
     def make():
         data = SiameseModelData(f)

@@ -1,5 +1,6 @@
 """Host mirror: flags + layer grammar, packer, feed-dict sampler pattern,
 C restatement vs numpy oracle.  CPU only."""
+import os
 import numpy as np
 import pytest
 
@@ -233,3 +234,62 @@ def test_validation_seed_stream_is_distinct():
                 assert not np.array_equal(mv, O.dropout_mask(model._seed(None), q, 0, 1, 320,
                                                              0.9)), (step, p, q)
     assert len(diffs) == 20   # no fixed key offset between the streams
+
+
+def test_default_loop_list_order_matches_reference_sampler():
+    """The host feed of the default loop (train_val, train.py:8-44: one train and one val
+    get_feed_dict per iteration, B + B² sampler calls each, A3) leaves the train and val
+    lists in the order the REFERENCE RandomSampler reaches after the same number of calls
+    (F7), so test()'s column j (get_orig_train_graph, A6) is the reference's."""
+    import json
+    from graphembedding_amd.config import Flags
+    from graphembedding_amd.data import synthetic_ged_matrix
+    from graphembedding_amd.data_siamese import SiameseModelData
+    from graphembedding_amd.dist_calculator import DistCalculator
+    from graphembedding_amd.model_mse import SiameseGCNTNMSE
+    with open(os.path.join(os.path.dirname(__file__), 'golden', 'f7_loop_lists.json')) as fh:
+        f7 = json.load(fh)
+    for iters in (1, 4, 20):
+        f = Flags(dataset='syn_aids80nef', node_feat_order='sorted', iters=iters)
+        data = SiameseModelData(f)
+        fresh = SiameseModelData(f)
+        gs = list(data.orig_train_graphs) + [data.test_data.gs[i].nxgraph for i in range(data.m)]
+        dc = DistCalculator.from_matrix(f.dataset, gs, synthetic_ged_matrix(gs))
+        model = SiameseGCNTNMSE(data.input_dim(), f, device='cpu')
+        for _ in range(iters):
+            model.get_feed_dict(data, dc, 'train')
+            model.get_feed_dict(data, dc, 'val')
+        for mine, orig in ((data.train_data, fresh.train_data),
+                           (data.valid_data, fresh.valid_data)):
+            ref = f7['random_{}_after_{}_calls'.format(len(orig.gs), 30 * iters)]
+            assert [g.nxgraph.graph['gid'] for g in mine.gs] == \
+                [orig.gs[k].nxgraph.graph['gid'] for k in ref['gs']], iters
+            assert mine.sampler.idx == ref['idx']
+
+
+def test_node_feat_order_set_vs_sorted():
+    """A7: 'set' keeps the reference's set iteration order (graphs.py:101-104), which for
+    string atom types depends on PYTHONHASHSEED; 'sorted' is the same map in every
+    process.  Two interpreters with different hash seeds, maps recorded."""
+    import json
+    import subprocess
+    import sys
+    code = ('import json,sys; sys.path.insert(0, {root!r}); '
+            'from graphembedding_amd.config import Flags; '
+            'from graphembedding_amd.data_siamese import SiameseModelData as D; '
+            'print(json.dumps([D(Flags(dataset="syn_aids80nef", node_feat_order=o))'
+            '.node_feat_encoder.feat_idx_dic for o in ("set", "sorted")]))').format(
+                root=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    maps = []
+    for hs in ('1', '2', '3'):
+        env = dict(os.environ, PYTHONHASHSEED=hs)
+        out = subprocess.run([sys.executable, '-c', code], env=env, check=True,
+                             capture_output=True, text=True).stdout
+        maps.append(json.loads(out.strip().splitlines()[-1]))
+    sets = [mp[0] for mp in maps]
+    sorts = [mp[1] for mp in maps]
+    assert sorts[0] == sorts[1] == sorts[2]
+    assert list(sorts[0]) == sorted(sorts[0], key=str)
+    assert all(sorted(s) == sorted(sorts[0]) for s in sets)   # same types, other columns
+    # the set order is the interpreter's own: string hashing differs across the seeds
+    assert len({tuple(s) for s in sets}) > 1, sets

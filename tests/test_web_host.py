@@ -107,6 +107,11 @@ def test_workspace_one_slot_for_single_chunk_calls():
     assert one == _lib.web_workspace_bytes(m, 4096, 0) and one < two
     # the slots dominate: the second one is most of the difference from the per-call part
     assert two - one > 0.4 * two
+    # chunk 0 = one chunk of the whole call (sg_web_run): sized for n_pairs, not for 1 pair
+    assert _lib.web_workspace_bytes(m, 0, 4096) == one
+    assert _lib.web_workspace_bytes(m, 0, 1) == _lib.web_workspace_bytes(m, 1, 1)
+    with pytest.raises(_lib.SiameseHipError):
+        _lib.web_workspace_bytes(m, 0)           # any n_pairs in chunk 0: not sizable
 
 
 def test_model_web_workspace_slots():
