@@ -103,7 +103,8 @@ def test_main_test_matrix_matches_oracle(gpu):
     fresh, cols = _expected_columns(f)
     assert [data.get_orig_train_graph(j).nxgraph.graph['gid'] for j in range(n)] == \
         [g.nxgraph.graph['gid'] for g in cols]
-    assert [g.nxgraph.graph['gid'] for g in data.orig_train_graphs] == \
+    # orig_train_graphs (networkx graphs) keep the load order: train list, then val list
+    assert [g.graph['gid'] for g in data.orig_train_graphs] == \
         [g.nxgraph.graph['gid'] for g in fresh.train_data.gs + fresh.valid_data.gs]
     seed = model._seed(None)                   # the eval launch's seed (no step since)
     g1s = [fresh.test_data.get_graph(i) for i in range(m) for _ in range(n)]
