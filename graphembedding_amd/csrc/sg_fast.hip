@@ -78,6 +78,11 @@ constexpr int W1TS = 36; // W1ᵀ table row stride (32 + pad)
 #endif
 // waves per block: 8 = 2 waves per SIMD at up to 256 VGPRs per lane
 constexpr int MAXW = SG_FAST_MAXW;
+// class-exclusive schedule: the waves that take one pair more than the others in their
+// class are the older waves of their SIMD pairs (1), or spread by the even split (0)
+#ifndef SG_LONG_OLD
+#define SG_LONG_OLD 1
+#endif
 
 struct FastArgs {
   const uint8_t *recs;
@@ -357,10 +362,28 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         if (cwave < 0 && gw < cum + wc[c]) {
-          const int k = gw - cum, nc = cb[c + 1] - cb[c];
+          const int nc = cb[c + 1] - cb[c];
           cwave = c;
+#if SG_LONG_OLD
+          // A class's nc slots over its wc waves: q or q + 1 each.  The r = nc % wc waves
+          // that take q + 1 are the OLDER waves of their SIMD pair (bit 2 of the grid wave
+          // index clear) first: the last pair of a long wave then tends to run beside a
+          // partner that has finished, at the single-wave rate, instead of beside another
+          // long wave (the launch tail is about one pair).  old(x) counts the older waves
+          // in [0, x).
+          auto old_below = [](int x) -> int { return (x >> 3) * 4 + min(x & 7, 4); };
+          const int end = cum + wc[c];
+          const int n_old = old_below(end) - old_below(cum);
+          const int k = (gw & 4) == 0 ? old_below(gw) - old_below(cum)
+                                      : n_old + (gw - old_below(gw)) - (cum - old_below(cum));
+          const int q = nc / wc[c], r = nc - q * wc[c];
+          cs0 = cb[c] + k * q + min(k, r);
+          cs1 = cs0 + q + (k < r ? 1 : 0);
+#else
+          const int k = gw - cum;
           cs0 = cb[c] + (int)((int64_t)k * nc / wc[c]);
           cs1 = cb[c] + (int)((int64_t)(k + 1) * nc / wc[c]);
+#endif
         }
         cum += wc[c];
       }

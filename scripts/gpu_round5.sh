@@ -1,0 +1,43 @@
+#!/bin/bash
+# Round-5 GPU session: the GPU suite + smoke on the product library, an alternating A/B of
+# C2 at N = 1 and at an emulated W = 8 rank (product library, variant libraries under ab/,
+# and class-weight settings through SG_CLS_W), then the driver's bench command with its
+# kernel-trace and PMC passes (scripts/gpu_round3.sh).  Usage:
+#   scripts/gpu_round5.sh TAG [skip-tests]    (variants: VARIANTS="ab/x.so ab/y.so",
+#                                              CLSW="1,1.315,1.316,1.493 ...")
+set -u
+TAG=${1:-r05}
+SKIP=${2:-}
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+if [ -z "$SKIP" ]; then
+  timeout -k 10 600 python -u -m pytest tests -v -m gpu --timeout 240 --timeout-method thread \
+    > "$OUT/pytest_gpu.log" 2>&1
+  rc=$?; echo "pytest_gpu rc=$rc" | tee -a "$OUT/summary.txt"; tail -3 "$OUT/pytest_gpu.log"
+  [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+  rc=$?; echo "smoke rc=$rc" | tee -a "$OUT/summary.txt"
+  [ $rc -eq 0 ] || exit $rc
+fi
+ab() {   # name, env-prefix..., -- bench args
+  local name=$1; shift
+  env "$@" timeout -k 10 300 python bench.py --cpu-sample -1 ${BENCH_ARGS_AB:-} \
+    --json-out "$OUT/ab_$name.json" > "$OUT/ab_$name.log" 2>&1
+  local rc=$?
+  [ $rc -eq 0 ] || { echo "ab $name rc=$rc" | tee -a "$OUT/summary.txt"; exit $rc; }
+  python -c "import json;d=json.load(open('$OUT/ab_$name.json'));print('$name', round(d['value']/1e6,2),'M pairs/s', round(d['ms_per_step'],5),'ms/step')" | tee -a "$OUT/summary.txt"
+}
+for rep in 1 2; do
+  for mode in n1 emu8; do
+    if [ $mode = n1 ]; then BENCH_ARGS_AB="--steps 40 --warmup 5"; else BENCH_ARGS_AB="--emulate-world 8 --steps 300 --warmup 30"; fi
+    ab "prod_${mode}_$rep" SG_NOP=1
+    for v in ${VARIANTS:-}; do ab "$(basename $v .so)_${mode}_$rep" SG_LIB=$ROOT/$v; done
+    k=0
+    for w in ${CLSW:-}; do k=$((k+1)); ab "clsw${k}_${mode}_$rep" SG_CLS_W=$w; done
+  done
+done
+bash scripts/gpu_round3.sh "$TAG" skip > "$OUT/round3.log" 2>&1
+rc=$?; echo "gpu_round3 rc=$rc" | tee -a "$OUT/summary.txt"
+exit $rc
