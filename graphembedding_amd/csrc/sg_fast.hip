@@ -1342,12 +1342,14 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   }
   __syncthreads();
   float *dst = A.slab + (size_t)blockIdx.x * (size_t)(A.n_params + 1);
-  for (int idx = tid; idx < NS * 64; idx += blockDim.x) {
-    const int prm_i = fast_param<D, AVG, ATT>(A, idx >> 6, idx & 63);
-    if (prm_i < 0) continue;
+  // wave wv sums slots wv, wv + nw, ...: the slot index is wave-uniform, so fast_param's
+  // region decode runs on scalar registers and only its lane part on VALU (the waves are
+  // summed in the same order as before: bitwise the same row)
+  for (int s = wv; s < NS; s += nw) {
+    const int prm_i = fast_param<D, AVG, ATT>(A, s, l);
     float acc = 0.f;
-    for (int w = 0; w < nw; ++w) acc += F[(size_t)w * NS * 64 + idx];
-    dst[prm_i] = acc;
+    for (int w = 0; w < nw; ++w) acc += F[((size_t)w * NS + s) * 64 + l];
+    if (prm_i >= 0) dst[prm_i] = acc;
   }
   SG_STAMP(3, __builtin_amdgcn_s_memrealtime());
 }
@@ -1514,7 +1516,7 @@ struct ClassWeights {
 };
 
 static ClassWeights class_weights_from_env() {
-  ClassWeights c = {{1.f, 1.29f, 1.31f, 1.47f}};
+  ClassWeights c = {{1.f, 1.315f, 1.316f, 1.493f}};
   if (const char *ev = getenv("SG_CLS_W")) {
     float w[4];
     if (sscanf(ev, "%f,%f,%f,%f", &w[0], &w[1], &w[2], &w[3]) == 4)
@@ -1556,7 +1558,10 @@ static int fast_run_impl(const sg_model_t *m, const SgGenPlan &P, bool bwd, cons
   A.cls = order ? class_start : nullptr;
   // relative cost of a pair of class (N0 > 8) + 2 (N1 > 8): the class-exclusive schedule
   // gives each class waves in proportion to count x cost (SG_CLS_W="w0,w1,w2,w3" to tune)
-  // (measured per-class µs/pair, scripts/fast_timing.py, profiles/r03_tim: 1, 1.29, 1.31, 1.47)
+  // (measured per-class µs/pair, scripts/fast_timing.py: profiles/r04_tim 1, 1.315, 1.311, 1.488
+  // at N = 1 and 1, 1.315, 1.316, 1.493 at an emulated W = 8 rank; round 5's A/B
+  // (profiles/r05_c): an emulated W = 8 rank 0.1338 / 0.1335 ms against 0.1345 / 0.1340 with
+  // the round-3 weights 1, 1.29, 1.31, 1.47, N = 1 within the box's spread)
   // (the environment is parsed once per process, and only for class-scheduled launches)
   if (A.cls) {
     static const ClassWeights cwt = class_weights_from_env();
