@@ -305,6 +305,17 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
     key = ((uint32_t)sd * 0x85EBCA6Bu) ^ (uint32_t)(sd >> 32);
   }
 
+  // the parameter staging's loads go out first: their latency overlaps the class table's
+  // and the order's (the first record waits for those: class table -> slot -> order entry)
+  float *stg = smem + A.shared_floats;   // fast_cfg sizes LDS for n_params floats here
+  const int nprm = A.n_params, bdx = (int)blockDim.x;
+  float stv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int i = k * bdx + tid;
+    stv[k] = i < nprm ? prm[i] : 0.f;
+  }
+
   // ---- pair schedule; the first record is loaded during the prologue ----
   // Slots are handed out round by round (round r: slots [r·S, r·S + S), S = all
   // waves of the grid).  With an order (sg_pair_order: records sorted by cost
@@ -410,15 +421,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
     ordA = load_ord(0);
     ordB = load_ord(64);
   }
-  // the parameter staging's loads go out together with the order's
-  float *stg = smem + A.shared_floats;   // fast_cfg sizes LDS for n_params floats here
-  const int nprm = A.n_params, bdx = (int)blockDim.x;
-  float stv[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int i = k * bdx + tid;
-    stv[k] = i < nprm ? prm[i] : 0.f;
-  }
 
   float *sW0 = smem;                            // W0 · ik0 · ik1, row d_in zero
   float *sWa = sW0 + (d_in + 1) * FH1;          // [a][k][12]: W[a][b][k] at b
@@ -510,7 +512,8 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #pragma unroll
   for (int k = 0; k < FK; ++k) usum += stg[A.oU + k];
   __syncthreads();   // the staging area is dead: the waves take their regions
-  for (int i = l; i < 2 * 16 * TS1; i += 64) sT[i] = 0.f;
+  static_assert((2 * 16 * TS1) % 4 == 0, "D1 tiles in float4s");
+  for (int i = l; i < 2 * 16 * TS1 / 4; i += 64) ((f4 *)sT)[i] = f4{0.f, 0.f, 0.f, 0.f};
   if (l < 48) sX[l] = 0.f;   // wave-private: the pair loop's first sg_wsync orders it
   SG_STAMP(1, __builtin_amdgcn_s_memrealtime());
 

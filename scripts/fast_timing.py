@@ -97,6 +97,16 @@ def main():
         young = us[w >= 4, 2] - us[w >= 4, 1]
         m = min(len(old), len(young))
         print('  young-old loop time', stats(young[:m] - old[:m]))
+        # the waves that end last, with their SIMD partner (w ^ 4 of the same block)
+        print('  last loop ends: wave (block, w, xcd) class pairs loop µs/pair | partner class '
+              'pairs loop-end')
+        for i in np.argsort(-us[:, 2])[:12]:
+            pi = (i // nwpb) * nwpb + ((i % nwpb) ^ 4)
+            pe = '{:2d} {:4d} {:8.2f}'.format(int(wcls[pi]), int(pairs[pi]), us[pi, 2]) \
+                if pi < nwv else '-'
+            print('    {:5d} ({:4d}, {}, {}) {:2d} {:4d} {:8.2f} {:5.2f} | {}'.format(
+                int(i), int(i // nwpb), int(i % nwpb), int(xcd[i]), int(wcls[i]), int(pairs[i]),
+                us[i, 2], per_pair[i], pe))
         sys.stdout.flush()
 
 
