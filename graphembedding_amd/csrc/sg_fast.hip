@@ -83,6 +83,11 @@ constexpr int MAXW = SG_FAST_MAXW;
 #ifndef SG_LONG_OLD
 #define SG_LONG_OLD 1
 #endif
+// ... and the two waves of a SIMD take the same class (1), or the classes are contiguous
+// ranges of the grid's wave index (0)
+#ifndef SG_PAIR_ALIGN
+#define SG_PAIR_ALIGN 1
+#endif
 
 struct FastArgs {
   const uint8_t *recs;
@@ -346,18 +351,25 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       tot += wt[c];
       nonempty += nc > 0;
     }
-    if (nonempty > 0 && stride >= nonempty) {
+    // SG_PAIR_ALIGN: the two waves of a SIMD (w and w ^ 4 of a block) always take the same
+    // class: the waves are allocated in SIMD pairs and enumerated block by block in the order
+    // (0, 4, 1, 5, 2, 6, 3, 7), so no SIMD runs pairs of two classes side by side (two
+    // classes' pair costs were fitted with partners of their own class)
+    const bool align = SG_PAIR_ALIGN && nw == 8;
+    const int units = align ? stride >> 1 : stride;
+    const int pos = align ? (gw & ~7) + 2 * (gw & 3) + ((gw >> 2) & 1) : gw;
+    if (nonempty > 0 && units >= nonempty) {
       int wc[4], used = 0;
       float fr[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const float x = wt[c] > 0.f ? (float)(stride - nonempty) * (wt[c] / tot) : 0.f;
+        const float x = wt[c] > 0.f ? (float)(units - nonempty) * (wt[c] / tot) : 0.f;
         const int fl = (int)x;
-        wc[c] = wt[c] > 0.f ? 1 + fl : 0;   // at least one wave per non-empty class
+        wc[c] = wt[c] > 0.f ? 1 + fl : 0;   // at least one unit per non-empty class
         fr[c] = x - (float)fl;
         used += wc[c];
       }
-      for (int left = stride - used; left > 0; --left) {   // largest remainders, ties to low c
+      for (int left = units - used; left > 0; --left) {   // largest remainders, ties to low c
         int bc = 0;
         float bf = -1.f;
 #pragma unroll
@@ -369,10 +381,14 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         wc[bc] += 1;
         fr[bc] = -2.f;
       }
+      if (align) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wc[c] *= 2;   // waves
+      }
       int cum = 0;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        if (cwave < 0 && gw < cum + wc[c]) {
+        if (cwave < 0 && pos < cum + wc[c]) {
           const int nc = cb[c + 1] - cb[c];
           cwave = c;
 #if SG_LONG_OLD
@@ -381,17 +397,22 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           // index clear) first: the last pair of a long wave then tends to run beside a
           // partner that has finished, at the single-wave rate, instead of beside another
           // long wave (the launch tail is about one pair).  old(x) counts the older waves
-          // in [0, x).
-          auto old_below = [](int x) -> int { return (x >> 3) * 4 + min(x & 7, 4); };
-          const int end = cum + wc[c];
-          const int n_old = old_below(end) - old_below(cum);
-          const int k = (gw & 4) == 0 ? old_below(gw) - old_below(cum)
-                                      : n_old + (gw - old_below(gw)) - (cum - old_below(cum));
+          // in [0, x) of the enumeration (every other position when aligned).
+          int k;
+          if (align) {
+            k = ((gw & 4) == 0 ? 0 : wc[c] >> 1) + ((pos - cum) >> 1);
+          } else {
+            auto old_below = [](int x) -> int { return (x >> 3) * 4 + min(x & 7, 4); };
+            const int end = cum + wc[c];
+            const int n_old = old_below(end) - old_below(cum);
+            k = (gw & 4) == 0 ? old_below(gw) - old_below(cum)
+                              : n_old + (gw - old_below(gw)) - (cum - old_below(cum));
+          }
           const int q = nc / wc[c], r = nc - q * wc[c];
           cs0 = cb[c] + k * q + min(k, r);
           cs1 = cs0 + q + (k < r ? 1 : 0);
 #else
-          const int k = gw - cum;
+          const int k = pos - cum;
           cs0 = cb[c] + (int)((int64_t)k * nc / wc[c]);
           cs1 = cb[c] + (int)((int64_t)(k + 1) * nc / wc[c]);
 #endif

@@ -38,6 +38,7 @@ for rep in 1 2; do
     for w in ${CLSW:-}; do k=$((k+1)); ab "clsw${k}_${mode}_$rep" SG_CLS_W=$w; done
   done
 done
+[ -n "${NO_ROUND3:-}" ] && exit 0
 bash scripts/gpu_round3.sh "$TAG" skip > "$OUT/round3.log" 2>&1
 rc=$?; echo "gpu_round3 rc=$rc" | tee -a "$OUT/summary.txt"
 exit $rc
