@@ -98,6 +98,11 @@ struct FastArgs {
   // waves split over the classes by work (count x cost weight cw[c])
   const int32_t *cls;
   float cw[4];
+  // relative pair throughput of the 8 XCDs (block b is assumed to run on XCD b % 8, which
+  // only decides speed: any placement gives the same results), scaled integers; a class's
+  // slots are split over its waves in proportion to their XCD's weight when the waves hold
+  // many pairs (SG_XCD_W)
+  int xw[8];
   int64_t n_pairs;
   int64_t pair_offset;
   int rw4h;      // 16-B words per HBM record (f32 or bf16 Â)
@@ -392,25 +397,48 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           const int nc = cb[c + 1] - cb[c];
           cwave = c;
 #if SG_LONG_OLD
-          // A class's nc slots over its wc waves: q or q + 1 each.  The r = nc % wc waves
-          // that take q + 1 are the OLDER waves of their SIMD pair (bit 2 of the grid wave
-          // index clear) first: the last pair of a long wave then tends to run beside a
-          // partner that has finished, at the single-wave rate, instead of beside another
-          // long wave (the launch tail is about one pair).  old(x) counts the older waves
-          // in [0, x) of the enumeration (every other position when aligned).
-          int k;
-          if (align) {
-            k = ((gw & 4) == 0 ? 0 : wc[c] >> 1) + ((pos - cum) >> 1);
-          } else {
-            auto old_below = [](int x) -> int { return (x >> 3) * 4 + min(x & 7, 4); };
-            const int end = cum + wc[c];
-            const int n_old = old_below(end) - old_below(cum);
-            k = (gw & 4) == 0 ? old_below(gw) - old_below(cum)
-                              : n_old + (gw - old_below(gw)) - (cum - old_below(cum));
-          }
+          // A class's nc slots over its wc waves.  Waves holding many pairs (N = 1 sizes)
+          // split them in proportion to their XCD's weight: the XCDs run the pair loop at
+          // measurably different speeds, the same on every box measured (profiles/r05_f,
+          // timing.log: XCD 3 and 7 the slowest, 0 and 4 the fastest), and the launch
+          // ends with the slowest XCD.  F(x) is the weight of the positions below x
+          // (8 positions per block, block b on XCD b % 8); the boundaries are integer
+          // quotients of cumulative weights, so the shares tile the class exactly.
           const int q = nc / wc[c], r = nc - q * wc[c];
-          cs0 = cb[c] + k * q + min(k, r);
-          cs1 = cs0 + q + (k < r ? 1 : 0);
+          if (q >= 64) {
+            auto F = [&](int x) -> int64_t {
+              const int xb = (x >> 3) & 7;
+              int64_t pre = 0, tot = 0;
+#pragma unroll
+              for (int i = 0; i < 8; ++i) {
+                tot += A.xw[i];
+                pre += i < xb ? A.xw[i] : 0;
+              }
+              return (int64_t)(x >> 6) * 8 * tot + 8 * pre + (int64_t)(x & 7) * A.xw[xb];
+            };
+            const int64_t f0 = F(cum), span = F(cum + wc[c]) - f0;
+            cs0 = cb[c] + (int)((int64_t)nc * (F(pos) - f0) / span);
+            cs1 = cb[c] + (int)((int64_t)nc * (F(pos + 1) - f0) / span);
+          } else {
+            // Few pairs per wave (an 8-GPU rank's share): q or q + 1 each, and the r = nc %
+            // wc waves that take q + 1 are the OLDER waves of their SIMD pair (bit 2 of the
+            // grid wave index clear) first: the last pair of a long wave then tends to run
+            // beside a partner that has finished, at the single-wave rate, instead of beside
+            // another long wave (the launch tail is about one pair).  old(x) counts the older
+            // waves in [0, x) of the enumeration (every other position when aligned).
+            int k;
+            if (align) {
+              k = ((gw & 4) == 0 ? 0 : wc[c] >> 1) + ((pos - cum) >> 1);
+            } else {
+              auto old_below = [](int x) -> int { return (x >> 3) * 4 + min(x & 7, 4); };
+              const int end = cum + wc[c];
+              const int n_old = old_below(end) - old_below(cum);
+              k = (gw & 4) == 0 ? old_below(gw) - old_below(cum)
+                                : n_old + (gw - old_below(gw)) - (cum - old_below(cum));
+            }
+            cs0 = cb[c] + k * q + min(k, r);
+            cs1 = cs0 + q + (k < r ? 1 : 0);
+          }
 #else
           const int k = pos - cum;
           cs0 = cb[c] + (int)((int64_t)k * nc / wc[c]);
@@ -1549,6 +1577,26 @@ static ClassWeights class_weights_from_env() {
   return c;
 }
 
+// Relative pair-loop speed of XCD x (block b on XCD b % 8), ×10^4: the inverse of the
+// median pair-loop end per XCD over four boxes, normalised (scripts/fast_timing.py at N = 1:
+// profiles/HISTORY.md's r04_tim, profiles/r05_d, r05_e, r05_f — XCD 0 .991, 1 1.005,
+// 2 1.000, 3 1.013, 4 .986, 5 .999, 6 .998, 7 1.009 of the mean).  SG_XCD_W="w0,...,w7"
+// replaces them (all equal: the even split).
+struct XcdWeights {
+  int w[8];
+};
+
+static XcdWeights xcd_weights_from_env() {
+  XcdWeights x = {{10089, 9949, 9999, 9875, 10145, 10014, 10017, 9915}};
+  if (const char *ev = getenv("SG_XCD_W")) {
+    int w[8];
+    if (sscanf(ev, "%d,%d,%d,%d,%d,%d,%d,%d", &w[0], &w[1], &w[2], &w[3], &w[4], &w[5], &w[6],
+               &w[7]) == 8)
+      for (int k = 0; k < 8; ++k) x.w[k] = w[k] > 0 ? w[k] : 10000;
+  }
+  return x;
+}
+
 int sg_ntn_wgrad_run(const float *ntn, int64_t n_pairs, int D, int oW, int oV, int obn, int C,
                      float *slab, int blocks, hipStream_t st);
 
@@ -1590,8 +1638,11 @@ static int fast_run_impl(const sg_model_t *m, const SgGenPlan &P, bool bwd, cons
   if (A.cls) {
     static const ClassWeights cwt = class_weights_from_env();
     for (int k = 0; k < 4; ++k) A.cw[k] = cwt.w[k];
+    static const XcdWeights xwt = xcd_weights_from_env();
+    for (int k = 0; k < 8; ++k) A.xw[k] = xwt.w[k];
   } else {
     for (int k = 0; k < 4; ++k) A.cw[k] = 1.f;
+    for (int k = 0; k < 8; ++k) A.xw[k] = 10000;
   }
   A.n_pairs = n_pairs;
   A.rw4h = P.hbm_words / 4;

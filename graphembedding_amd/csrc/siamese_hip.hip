@@ -80,21 +80,18 @@ __global__ void __launch_bounds__(256) sg_reduce_stage1(const float *__restrict_
 }
 
 // slab [nblk][C] → grad[C-1], loss in one pass (nblk <= kOnePassRows): block x owns
-// columns 16x .. 16x+15; thread (w, c) of 16 x 16 sums rows w + 16 i of column c into four
-// independent partials (i mod 4), combined in fixed order, and the 16 partials of a column
-// are summed in order w = 0..15 (deterministic).  16 columns per 256-thread block put the
-// reduction on ≈171 CUs at C = 2,726 (one memory latency per 256 rows on each) instead of
-// 43 blocks of 1,024 threads; the arithmetic of every column is unchanged.
-constexpr int kRedCols = 16;
-__global__ void __launch_bounds__(256) sg_reduce_one(const float *__restrict__ slab, int nblk, int C,
-                                                     float *__restrict__ grad,
-                                                     float *__restrict__ loss,
-                                                     const float *__restrict__ y_stats,
-                                                     int add_label) {
-  __shared__ float red[16][kRedCols];
-  const int c = threadIdx.x & (kRedCols - 1), w = threadIdx.x / kRedCols;
-  const int col = blockIdx.x * kRedCols + c;
-  // rows w + 16 k in a fixed order; 16 rows per batch with every load in flight
+// columns 64x .. 64x+63; wave w of 16 sums rows w + 16 i into four independent
+// partials (i mod 4), combined in fixed order (deterministic)
+__global__ void __launch_bounds__(1024) sg_reduce_one(const float *__restrict__ slab, int nblk, int C,
+                                                      float *__restrict__ grad,
+                                                      float *__restrict__ loss,
+                                                      const float *__restrict__ y_stats,
+                                                      int add_label) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  // wave w sums rows w + 16 k in a fixed order; 16 rows per batch with every load
+  // in flight (one memory latency per 256 slab rows)
   float a[4] = {0.f, 0.f, 0.f, 0.f};
   if (col < C) {
     const float *p = slab + col;
@@ -108,12 +105,12 @@ __global__ void __launch_bounds__(256) sg_reduce_one(const float *__restrict__ s
     }
     for (; b < nblk; b += 16) a[0] += p[(size_t)b * C];
   }
-  red[w][c] = (a[0] + a[1]) + (a[2] + a[3]);
+  red[w][lane] = (a[0] + a[1]) + (a[2] + a[3]);
   __syncthreads();
   if (w == 0 && col < C) {
     float v = 0.f;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v += red[k][c];
+    for (int k = 0; k < 16; ++k) v += red[k][lane];
     if (col < C - 1)
       grad[col] = v;
     else if (loss)
@@ -447,8 +444,8 @@ __global__ void __launch_bounds__(64) sg_adam_final(const double *__restrict__ p
 int launch_reduce(const float *slab, int nblk, int C, float *part, float *grad, float *loss,
                   const float *y_stats, int add_label, hipStream_t st) {
   if (nblk <= kOnePassRows) {   // the fused kernel's one-block-per-CU slabs
-    hipLaunchKernelGGL(sg_reduce_one, dim3((C + kRedCols - 1) / kRedCols), dim3(256), 0, st, slab,
-                       nblk, C, grad, loss, y_stats, add_label);
+    hipLaunchKernelGGL(sg_reduce_one, dim3((C + 63) / 64), dim3(1024), 0, st, slab, nblk, C, grad,
+                       loss, y_stats, add_label);
     return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
   }
   const int S = nblk < kReduceStrands ? (nblk > 0 ? nblk : 1) : kReduceStrands;

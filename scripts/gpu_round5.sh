@@ -4,7 +4,8 @@
 # and class-weight settings through SG_CLS_W), then the driver's bench command with its
 # kernel-trace and PMC passes (scripts/gpu_round3.sh).  Usage:
 #   scripts/gpu_round5.sh TAG [skip-tests]    (variants: VARIANTS="ab/x.so ab/y.so",
-#                                              CLSW="1,1.315,1.316,1.493 ...")
+#                                              CLSW="1,1.315,1.316,1.493 ...",
+#                                              XCDW="10000,10000,... (8) ...")
 set -u
 TAG=${1:-r05}
 SKIP=${2:-}
@@ -36,6 +37,8 @@ for rep in 1 2; do
     for v in ${VARIANTS:-}; do ab "$(basename $v .so)_${mode}_$rep" SG_LIB=$ROOT/$v; done
     k=0
     for w in ${CLSW:-}; do k=$((k+1)); ab "clsw${k}_${mode}_$rep" SG_CLS_W=$w; done
+    k=0
+    for w in ${XCDW:-}; do k=$((k+1)); ab "xcdw${k}_${mode}_$rep" SG_XCD_W=$w; done
   done
 done
 [ -n "${NO_ROUND3:-}" ] && exit 0
