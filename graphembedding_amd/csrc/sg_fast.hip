@@ -1577,17 +1577,18 @@ static ClassWeights class_weights_from_env() {
   return c;
 }
 
-// Relative pair-loop speed of XCD x (block b on XCD b % 8), ×10^4: the inverse of the
-// median pair-loop end per XCD over four boxes, normalised (scripts/fast_timing.py at N = 1:
-// profiles/HISTORY.md's r04_tim, profiles/r05_d, r05_e, r05_f — XCD 0 .991, 1 1.005,
-// 2 1.000, 3 1.013, 4 .986, 5 .999, 6 .998, 7 1.009 of the mean).  SG_XCD_W="w0,...,w7"
-// replaces them (all equal: the even split).
+// Relative pair-loop speed of XCD x (block b on XCD b % 8), ×10^4.  The default is equal
+// weights (the even split).  Measured and not adopted (profiles/r05_g): weights from the
+// median pair-loop end per XCD on four boxes (XCD 0 .991, 1 1.005, 2 1.000, 3 1.013,
+// 4 .986, 5 .999, 6 .998, 7 1.009 of the mean time) ran 546.4 / 546.9 against 546.0 / 548.5
+// M pairs/s: on a fifth box only XCD 3 (slow) and 4 (fast) kept their place, and XCD 0,
+// given more pairs, ended last.  SG_XCD_W="w0,...,w7" sets them.
 struct XcdWeights {
   int w[8];
 };
 
 static XcdWeights xcd_weights_from_env() {
-  XcdWeights x = {{10089, 9949, 9999, 9875, 10145, 10014, 10017, 9915}};
+  XcdWeights x = {{10000, 10000, 10000, 10000, 10000, 10000, 10000, 10000}};
   if (const char *ev = getenv("SG_XCD_W")) {
     int w[8];
     if (sscanf(ev, "%d,%d,%d,%d,%d,%d,%d,%d", &w[0], &w[1], &w[2], &w[3], &w[4], &w[5], &w[6],
