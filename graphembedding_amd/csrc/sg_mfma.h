@@ -40,8 +40,13 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {   // v_cvt_pk_bf
 __device__ __forceinline__ uint32_t hi16x2(uint32_t a, uint32_t b) {   // hi16(a) | hi16(b) << 16
   return __builtin_amdgcn_perm(b, a, 0x07060302u);
 }
+// SG_SPLIT_PK = 1: the two residual subtractions of each level as one v_pk_add_f32.  It
+// measured +0.1% in round 2; on the round-5 kernels the packed operands cost register
+// copies (11 v_mov_b32 in the (2, 2) class loop of sg_fast) and the plain subtractions run
+// C2 at 558.5 / 561.7 against 550.9 / 552.6 M pairs/s (profiles/r05_k, same box).  Both
+// forms compute the same IEEE subtractions: the parts are bitwise the same.
 #ifndef SG_SPLIT_PK
-#define SG_SPLIT_PK 1
+#define SG_SPLIT_PK 0
 #endif
 __device__ __forceinline__ void split3(float x0, float x1, uint32_t &h, uint32_t &m, uint32_t &l) {
   const uint32_t u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);

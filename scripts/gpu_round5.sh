@@ -5,7 +5,8 @@
 # kernel-trace and PMC passes (scripts/gpu_round3.sh).  Usage:
 #   scripts/gpu_round5.sh TAG [skip-tests]    (variants: VARIANTS="ab/x.so ab/y.so",
 #                                              CLSW="1,1.315,1.316,1.493 ...",
-#                                              XCDW="10000,10000,... (8) ...")
+#                                              XCDW="10000,10000,... (8) ...",
+#                                              MODES="n1 emu8 c4 c5 c3 avg att")
 set -u
 TAG=${1:-r05}
 SKIP=${2:-}
@@ -31,8 +32,16 @@ ab() {   # name, env-prefix..., -- bench args
   python -c "import json;d=json.load(open('$OUT/ab_$name.json'));print('$name', round(d['value']/1e6,2),'M pairs/s', round(d['ms_per_step'],5),'ms/step')" | tee -a "$OUT/summary.txt"
 }
 for rep in 1 2; do
-  for mode in n1 emu8; do
-    if [ $mode = n1 ]; then BENCH_ARGS_AB="--steps 40 --warmup 5"; else BENCH_ARGS_AB="--emulate-world 8 --steps 300 --warmup 30"; fi
+  for mode in ${MODES:-n1 emu8}; do
+    case $mode in
+      n1) BENCH_ARGS_AB="--steps 40 --warmup 5" ;;
+      emu8) BENCH_ARGS_AB="--emulate-world 8 --steps 300 --warmup 30" ;;
+      c4) BENCH_ARGS_AB="--dataset syn_aids10knef --steps 2 --warmup 1" ;;
+      c5) BENCH_ARGS_AB="--dataset syn_web --steps 3 --warmup 1" ;;
+      c3) BENCH_ARGS_AB="--records bf16 --steps 40 --warmup 5" ;;
+      avg) BENCH_ARGS_AB="--stack average --steps 40 --warmup 5" ;;
+      att) BENCH_ARGS_AB="--stack attention --steps 40 --warmup 5" ;;
+    esac
     ab "prod_${mode}_$rep" SG_NOP=1
     for v in ${VARIANTS:-}; do ab "$(basename $v .so)_${mode}_$rep" SG_LIB=$ROOT/$v; done
     k=0
