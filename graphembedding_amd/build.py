@@ -45,10 +45,13 @@ def _stale() -> bool:
 # ILP (max-ilp: +1.2%; the capacity-32 kernel measured 0.8% slower with it), the
 # capacity-32 kernel with the AMDGPU register-pressure trackers (+0.5%), the graph-store
 # (C5) kernels for ILP (+1.0%: 4.006 vs 3.965 M pairs/s, profiles/r03_c5ab/)
+# (the capacity-32 and graph-store kernels keep the packed split3 residuals, SG_SPLIT_PK=1:
+# C4 152.5 / 152.3 against 151.6 / 151.9 M pairs/s without, C5 4.85 / 4.84 against 4.84 /
+# 4.83; sg_fast runs 1.7% faster without them, profiles/r05_l)
 SOURCE_FLAGS = {'sg_fast.hip': ['-mllvm', '-amdgpu-sched-strategy=max-ilp'],
                 'sg_fast_att.hip': ['-mllvm', '-amdgpu-sched-strategy=max-ilp'],
-                'sg_fast32.hip': ['-mllvm', '-amdgpu-use-amdgpu-trackers'],
-                'sg_web.hip': ['-mllvm', '-amdgpu-sched-strategy=max-ilp']}
+                'sg_fast32.hip': ['-mllvm', '-amdgpu-use-amdgpu-trackers', '-DSG_SPLIT_PK=1'],
+                'sg_web.hip': ['-mllvm', '-amdgpu-sched-strategy=max-ilp', '-DSG_SPLIT_PK=1']}
 
 
 def build_hip(force: bool = False, verbose: bool = False, out: str = None, defines=()) -> str:
