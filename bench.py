@@ -68,6 +68,14 @@ def parse():
     p.add_argument('--settle-ms', type=float, default=60.0,
                    help='untimed forward-only launches on the resident batch for at least this '
                         'long before the warmup steps (GPU clock settle; 0: none)')
+    p.add_argument('--events', choices=('timed', 'after'), default='after',
+                   help='where the HIP events around the step\'s kernels (the roofline\'s '
+                        'kernel time) are recorded: on as many extra steps right after the '
+                        'timed region (default), or on every timed step (the two timing '
+                        'events of a step add ≈8 µs of dispatch gaps to it, profiles/r05_n)')
+    p.add_argument('--no-fused-adam', action='store_true',
+                   help='N = 1: run the gradient reduction and Adam as two launches '
+                        '(sg_fwd_bwd + sg_adam_tf) instead of sg_train_step')
     p.add_argument('--json-out', default='')
     p.add_argument('--emulate-world', type=int, default=0,
                    help='diagnostic: time rank 0\'s share of a W-GPU step on one GPU (no collective)')
@@ -300,6 +308,8 @@ def main():
         prep = {'order_ms': e0.elapsed_time(e1)}
 
     ev = []
+    fuse_adam = not args.no_fused_adam and model.kernel_path == 1 and batch is not None and \
+        batch.csr is None and batch.src is None
 
     def step(timed):
         if timed:
@@ -308,14 +318,19 @@ def main():
             e0.record(stream)
         if streamed:
             shard.fwd_bwd(model, add_label_term=(rank == 0))
+        elif hook is None and fuse_adam:
+            # one process: the gradient reduction applies Adam in the same launch
+            # (sg_train_step); N > 1 all-reduces the gradient between the two
+            model.fwd_bwd_adam(batch, add_label_term=(rank == 0))
         else:
             model.fwd_bwd(batch, add_label_term=(rank == 0))
         if timed:
             e1.record(stream)
             ev.append((e0, e1))
-        if hook is not None:
-            hook(model)
-        model.apply_adam()
+        if streamed or hook is not None or not fuse_adam:
+            if hook is not None:
+                hook(model)
+            model.apply_adam()
         model.step_count += 1
 
     # GPU clock settle (untimed, before the warmup steps): after the host-side setup the
@@ -342,12 +357,16 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(True)
+        step(args.events == 'timed')
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if args.events == 'after':
+        for _ in range(args.steps):
+            step(True)
+        torch.cuda.synchronize()
     params_agree = None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -479,6 +498,8 @@ def main():
                        'settle_ms': round(settle_ms, 1),
                        'inputs': inputs,
                        'parallelism': 'dp{}'.format(world),
+                       'adam': ('in the gradient reduction\'s launch (sg_train_step)'
+                                if (fuse_adam and hook is None) else 'sg_adam_tf launch'),
                        'collective': ('{} all-reduce of the flat gradient + loss ({} B)'.format(
                            'ncclAllReduce on the compute stream' if collective == 'rccl' else
                            'torch.distributed', 4 * (model.grad.numel() + 1))
@@ -488,10 +509,16 @@ def main():
                          'traffic': traffic, 'traffic_source': traffic_src,
                          'note': 'fp32 compute roof (gfx950 vector fp32 == f32 MFMA peak); '
                                  'algorithmic {:.0f} FLOP/pair x {} pairs per launch / {} '
-                                 'event time {:.3f} ms'.format(
+                                 'event time {:.3f} ms ({})'.format(
                                      flops_pair, shard.n,
-                                     'sg_web_fwd_bwd (all its kernels)' if web else 'sg_fwd_bwd',
-                                     kern_ms)},
+                                     'sg_web_fwd_bwd (all its kernels)' if web else
+                                     ('sg_train_step (fused kernel, then the gradient reduction '
+                                      'with Adam)' if (fuse_adam and hook is None) else
+                                      'sg_fwd_bwd'),
+                                     kern_ms, 'events on every timed step'
+                                     if args.events == 'timed' else
+                                     'events on {} steps right after the timed region'.format(
+                                         args.steps))},
             'roofline_hbm': {'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                              'frac': achieved_gbs / HBM_PEAK_GBS,
                              'bytes_per_pair': bytes_pair},

@@ -24,6 +24,15 @@
 // ---------------------------------------------------------------------------
 // 24-bit-multiply lowbias32 variant: (x & 0xFFFFFF) * C is one full-rate
 // v_mul_u32_u24 on gfx950.
+// sg_train_step: what the fused kernel's block 0 needs to compute ApplyAdam's step
+// scalars out[4] = {α, β1^t·β1, β2^t·β2, wd·½Σθ²} before the reduction launch applies the
+// update (host struct, copied into the kernel arguments)
+struct SgAdamPre {
+  const float *bp;   // device [2] β powers {β1^t, β2^t}
+  float *out;        // device [4]
+  float lr, b1, b2, wd;
+};
+
 __host__ __device__ __forceinline__ uint32_t sg_mix(uint32_t x) {
   x ^= x >> 16;
   x = (x & 0xFFFFFFu) * 0x7FEB35u;

@@ -116,6 +116,12 @@ struct FastArgs {
   uint32_t key;
   const uint64_t *seed_dev;   // non-null: the dropout seed is read from device memory
                               // (graph-captured steps, sg_fwd_bwd_dseed)
+  // sg_train_step (backward, ad_out non-null): block 0 computes ApplyAdam's step scalars
+  // from the parameters it stages, ad_out[4] = {α, β1^t·β1, β2^t·β2, wd·½Σθ²} with
+  // β^t = ad_bp[0..1], so that the reduction launch's blocks (sg_reduce_adam) only read them
+  const float *ad_bp;
+  float *ad_out;
+  float ad_lr, ad_b1, ad_b2, ad_wd;
   uint32_t thr0, thr1, thr2, thr4;
   float ik0, ik1, ik2, ik4;
   float yeta;
@@ -260,6 +266,21 @@ __device__ __forceinline__ int fast_param(const FastArgs &A, int s, int l) {
   return (ATT && s < 4) ? A.oWa + (4 * s + g) * FH2 + j : -1;
 }
 
+// The NTN head's FMAs over element pairs (b, b + 1): one v_pk_fma_f32 (SG_NTN_PK = 1) or
+// two v_fma_f32 (0); the same two fmaf chains either way, so the results are bitwise equal.
+// Unlike split3's packed subtractions (SG_SPLIT_PK), these keep their register pairs: the
+// plain form measured 1.1% slower on C2 and 0.7% at an emulated W = 8 rank (profiles/r05_n).
+#ifndef SG_NTN_PK
+#define SG_NTN_PK 1
+#endif
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) {
+#if SG_NTN_PK
+  return __builtin_elementwise_fma(a, b, c);
+#else
+  return f2{fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y)};
+#endif
+}
+
 // tanh and the logistic function from v_exp_f32 and v_rcp_f32 (the Attention layer's h
 // and att, layers.py:156-157).  Both are ≈1e-7 ABSOLUTE error: sg_tanh's 1 - 2/(e^2z + 1)
 // cancels for small |z| (relative error ≈1e-7/|z|, e.g. 1e-3 at |z| = 1e-4), which the
@@ -324,6 +345,12 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   for (int k = 0; k < 8; ++k) {
     const int i = k * bdx + tid;
     stv[k] = i < nprm ? prm[i] : 0.f;
+  }
+  const bool ad_blk = BWD && A.ad_out != nullptr && blockIdx.x == 0 && wv == 0;
+  float ad_b1p = 0.f, ad_b2p = 0.f;
+  if (ad_blk) {
+    ad_b1p = A.ad_bp[0];
+    ad_b2p = A.ad_bp[1];
   }
 
   // ---- pair schedule; the first record is loaded during the prologue ----
@@ -515,6 +542,21 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
                  : uint4{0u, 0u, 0u, 0u};
   }
   __syncthreads();
+  if (ad_blk) {   // sg_train_step's step scalars (see FastArgs::ad_out), from the staged θ
+    double ss = 0.0;
+    for (int i = l; i < nprm; i += 64) {
+      const double t = (double)stg[i];
+      ss += t * t;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    if (l == 0) {
+      A.ad_out[0] = A.ad_lr * sqrtf(1.f - ad_b2p) / (1.f - ad_b1p);
+      A.ad_out[1] = ad_b1p * A.ad_b1;
+      A.ad_out[2] = ad_b2p * A.ad_b2;
+      A.ad_out[3] = (float)((double)A.ad_wd * 0.5 * ss);
+    }
+  }
   for (int i = tid; i < (d_in + 1) * FH1; i += blockDim.x)
     sW0[i] = i < d_in * FH1 ? stg[A.oW0 + i] * (A.ik0 * A.ik1) : 0.f;
   for (int i = tid; i < DN * FK * WR; i += blockDim.x) {
@@ -988,7 +1030,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           f2 acc2 = {0.f, 0.f};
 #pragma unroll
           for (int b = 0; b < BP1; ++b)
-            acc2 = __builtin_elementwise_fma(*(const f2 *)(wa + 2 * b), x2[b], acc2);
+            acc2 = pfma(*(const f2 *)(wa + 2 * b), x2[b], acc2);
           const float acc = acc2.x + acc2.y;
           u[r] = acc;
           // x1[a] u[a][k] + V[k][a] x1[a] + V[k][D+a] x2[a]   (x of invalid a is 0)
@@ -1050,7 +1092,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
               const float c = gmk * xo[0][r];
               const f2 c2 = {c, c};
 #pragma unroll
-              for (int b = 0; b < BP1; ++b) gWn[r][b] = __builtin_elementwise_fma(c2, x2[b], gWn[r][b]);
+              for (int b = 0; b < BP1; ++b) gWn[r][b] = pfma(c2, x2[b], gWn[r][b]);
               gVa[r] = fmaf(gmk, xo[0][r], gVa[r]);
             }
             tt[r] = gmk4 * (sV[kc * VS + ac] + u[r]);
@@ -1061,7 +1103,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
             f2 w2 = {0.f, 0.f};
 #pragma unroll
             for (int aa = 0; aa < BP0; ++aa)
-              w2 = __builtin_elementwise_fma(x1[aa], *(const f2 *)(wb + 2 * aa), w2);
+              w2 = pfma(x1[aa], *(const f2 *)(wb + 2 * aa), w2);
             const float w = w2.x + w2.y;
             tt[RA + r] = gmk4 * (sV[kc * VS + DN + ac] + w);
           }
@@ -1609,7 +1651,8 @@ static int fast_run_impl(const sg_model_t *m, const SgGenPlan &P, bool bwd, cons
                          int64_t batch_total, const float *params, uint64_t seed,
                          const float *y_stats, float *s_out, float *slab, float *ntn,
                          int *blocks_out, hipStream_t stream, const uint64_t *seed_dev,
-                         const sg_pair_source_t *src, const int32_t *class_start) {
+                         const sg_pair_source_t *src, const int32_t *class_start,
+                         const SgAdamPre *adam_pre) {
   const int D = P.n_max;
   FastCfg c = fast_cfg(P, n_pairs, bwd);
   // the kernel indexes pairs in 32 bits (2^31 records would be ≥ 1 TB)
@@ -1656,6 +1699,17 @@ static int fast_run_impl(const sg_model_t *m, const SgGenPlan &P, bool bwd, cons
   A.ntn = ntn;
   A.key = sg_seed_key(seed);
   A.seed_dev = seed_dev;
+  A.ad_bp = nullptr;
+  A.ad_out = nullptr;
+  A.ad_lr = A.ad_b1 = A.ad_b2 = A.ad_wd = 0.f;
+  if (bwd && adam_pre != nullptr) {
+    A.ad_bp = adam_pre->bp;
+    A.ad_out = adam_pre->out;
+    A.ad_lr = adam_pre->lr;
+    A.ad_b1 = adam_pre->b1;
+    A.ad_b2 = adam_pre->b2;
+    A.ad_wd = adam_pre->wd;
+  }
   const float keep = m->keep_prob;
   const bool avg = plan_avg(P);   // NTN is layer 3 after Average / Attention
   const bool att = plan_att(P);
@@ -1719,9 +1773,10 @@ int sg_fast_att_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const voi
                     int64_t batch_total, const float *params, uint64_t seed,
                     const float *y_stats, float *s_out, float *slab, float *ntn, int *blocks_out,
                     hipStream_t stream, const uint64_t *seed_dev, const sg_pair_source_t *src,
-                    const int32_t *class_start) {
+                    const int32_t *class_start, const SgAdamPre *adam_pre) {
   return fast_run_impl(m, P, bwd, recs, order, n_pairs, pair_offset, batch_total, params, seed,
-                       y_stats, s_out, slab, ntn, blocks_out, stream, seed_dev, src, class_start);
+                       y_stats, s_out, slab, ntn, blocks_out, stream, seed_dev, src, class_start,
+                       adam_pre);
 }
 #else
 int sg_fast_att_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *recs,
@@ -1729,7 +1784,7 @@ int sg_fast_att_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const voi
                     int64_t batch_total, const float *params, uint64_t seed,
                     const float *y_stats, float *s_out, float *slab, float *ntn, int *blocks_out,
                     hipStream_t stream, const uint64_t *seed_dev, const sg_pair_source_t *src,
-                    const int32_t *class_start);
+                    const int32_t *class_start, const SgAdamPre *adam_pre);
 
 int sg_fast_supported(const sg_model_t *m, const SgGenPlan &P) {
   if (getenv("SG_DISABLE_FAST")) return 0;
@@ -1748,13 +1803,14 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
                 const float *params, uint64_t seed, const float *y_stats, float *s_out,
                 float *slab, float *ntn, int *blocks_out, hipStream_t stream,
                 const uint64_t *seed_dev, const sg_pair_source_t *src,
-                const int32_t *class_start) {
+                const int32_t *class_start, const SgAdamPre *adam_pre) {
   if (plan_att(P))
     return sg_fast_att_run(m, P, bwd, recs, order, n_pairs, pair_offset, batch_total, params,
                            seed, y_stats, s_out, slab, ntn, blocks_out, stream, seed_dev, src,
-                           class_start);
+                           class_start, adam_pre);
   return fast_run_impl(m, P, bwd, recs, order, n_pairs, pair_offset, batch_total, params, seed,
-                       y_stats, s_out, slab, ntn, blocks_out, stream, seed_dev, src, class_start);
+                       y_stats, s_out, slab, ntn, blocks_out, stream, seed_dev, src, class_start,
+                       adam_pre);
 }
 #endif
 

@@ -37,7 +37,8 @@ int sg_fast_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void *r
                 const int32_t *order, int64_t n_pairs, int64_t pair_offset, int64_t batch_total, const float *params,
                 uint64_t seed, const float *y_stats, float *s_out, float *slab, float *ntn,
                 int *blocks_out, hipStream_t stream, const uint64_t *seed_dev = nullptr,
-                const sg_pair_source_t *src = nullptr, const int32_t *class_start = nullptr);
+                const sg_pair_source_t *src = nullptr, const int32_t *class_start = nullptr,
+                const SgAdamPre *adam_pre = nullptr);
 // fused capacity-32 path (sg_fast32.hip)
 int sg_fast32_supported(const sg_model_t *m, const SgGenPlan &P);
 // graph-store path for Web-sized graphs (sg_web.hip)
@@ -62,6 +63,17 @@ namespace {
 
 constexpr int kReduceStrands = 16;  // second-level partial rows
 constexpr int kOnePassRows = 1024;  // slabs up to this many rows reduce in one launch
+
+// TF ApplyAdam of one element (+ the weight-decay gradient, models.py:67-73): one
+// expression for every Adam kernel, so that they contract it alike (bitwise the same θ, m,
+// v from sg_adam_tf, sg_adam_tf_ex and sg_train_step)
+__device__ __forceinline__ float adam_elem(float tv, float gv, float &mv, float &vv, float wd,
+                                           float c1, float c2, float alpha, float eps) {
+  const float gi = gv + wd * tv;
+  mv = mv + (gi - mv) * c1;
+  vv = vv + (gi * gi - vv) * c2;
+  return tv - (mv * alpha) / (sqrtf(vv) + eps);
+}
 
 // slab [nblk][C] → part [S][C]; strand order fixed ⇒ bitwise reproducible.
 __global__ void __launch_bounds__(256) sg_reduce_stage1(const float *__restrict__ slab, int nblk,
@@ -115,6 +127,66 @@ __global__ void __launch_bounds__(1024) sg_reduce_one(const float *__restrict__ 
       grad[col] = v;
     else if (loss)
       loss[0] = v + ((add_label && y_stats) ? y_stats[1] : 0.f);
+  }
+}
+
+// sg_reduce_one + the update of sg_adam_kernel in one launch (sg_train_step): block x
+// reduces columns 64x .. 64x+63 of the slab exactly as sg_reduce_one (grad, loss), then
+// wave 0 applies ApplyAdam to those parameters (adam_elem).  The step scalars pre[4] =
+// {α, β1^t·β1, β2^t·β2, wd·½Σθ²} come from the fused kernel's block 0 (FastArgs::ad_out),
+// so no block waits on another: block 0 stores the new β powers and reg_loss.
+__global__ void __launch_bounds__(1024) sg_reduce_adam(
+    const float *__restrict__ slab, int nblk, int C, float *__restrict__ grad,
+    float *__restrict__ loss, const float *__restrict__ y_stats, int add_label,
+    float *__restrict__ th, float *__restrict__ m, float *__restrict__ v, float b1, float b2,
+    float eps, float wd, const float *__restrict__ pre, float *__restrict__ bp,
+    float *__restrict__ reg_loss) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
+  const int n = C - 1;
+  // wave 0's Adam operands: loaded first, their latency under the slab's
+  float tv = 0.f, mv = 0.f, vv = 0.f, alpha = 0.f;
+  if (w == 0) {
+    alpha = pre[0];
+    if (col < n) {
+      tv = th[col];
+      mv = m[col];
+      vv = v[col];
+    }
+  }
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  if (col < C) {
+    const float *p = slab + col;
+    int b = w;
+    for (; b + 16 * 15 < nblk; b += 256) {
+      float x[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) x[k] = p[(size_t)(b + 16 * k) * C];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) a[k & 3] += x[k];
+    }
+    for (; b < nblk; b += 16) a[0] += p[(size_t)b * C];
+  }
+  red[w][lane] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (w != 0) return;
+  float gsum = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) gsum += red[k][lane];
+  if (col < n) {
+    grad[col] = gsum;
+    const float ti = adam_elem(tv, gsum, mv, vv, wd, 1.f - b1, 1.f - b2, alpha, eps);
+    m[col] = mv;
+    v[col] = vv;
+    th[col] = ti;
+  } else if (col == n && loss) {
+    loss[0] = gsum + ((add_label && y_stats) ? y_stats[1] : 0.f);
+  }
+  if (blockIdx.x == 0 && lane == 0) {
+    bp[0] = pre[1];
+    bp[1] = pre[2];
+    if (reg_loss) reg_loss[0] = pre[3];
   }
 }
 
@@ -372,12 +444,11 @@ __global__ void __launch_bounds__(1024) sg_adam_kernel(float *__restrict__ th, f
       const int64_t i = base + k * 1024 + t;
       if (i < n) {
         reg += (double)tv[k] * (double)tv[k];
-        const float gi = gv[k] + wd * tv[k];
-        const float mi = mv[k] + (gi - mv[k]) * c1;
-        const float vi = vv[k] + (gi * gi - vv[k]) * c2;
+        float mi = mv[k], vi = vv[k];
+        const float ti = adam_elem(tv[k], gv[k], mi, vi, wd, c1, c2, alpha, eps);
         m[i] = mi;
         v[i] = vi;
-        th[i] = tv[k] - (mi * alpha) / (sqrtf(vi) + eps);
+        th[i] = ti;
       }
     }
   }
@@ -412,12 +483,11 @@ __global__ void __launch_bounds__(256) sg_adam_multi(float *__restrict__ th, flo
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const float tv = th[i];
     reg += (double)tv * (double)tv;
-    const float gi = g[i] + wd * tv;
-    const float mi = m[i] + (gi - m[i]) * c1;
-    const float vi = v[i] + (gi * gi - v[i]) * c2;
+    float mi = m[i], vi = v[i];
+    const float ti = adam_elem(tv, g[i], mi, vi, wd, c1, c2, alpha, eps);
     m[i] = mi;
     v[i] = vi;
-    th[i] = tv - (mi * alpha) / (sqrtf(vi) + eps);
+    th[i] = ti;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) reg += __shfl_xor(reg, o);
@@ -505,7 +575,7 @@ int64_t ntn_offset_floats(const PathChoice &c, int64_t n_pairs) {
 // ===========================================================================
 extern "C" {
 
-int32_t sg_version(void) { return 10800; }   /* 1.8.0: sg_web_workspace_bytes_ex; fused Attention pooling */
+int32_t sg_version(void) { return 10900; }   /* 1.9.0: sg_train_step (gradient reduction + Adam in one launch) */
 
 int64_t sg_record_bytes(int32_t n_max) { return sg_record_bytes_ex(n_max, SG_DTYPE_F32); }
 
@@ -737,7 +807,8 @@ static int32_t fwd_bwd_impl(const sg_model_t *model, const void *records, const 
                             const float *y_stats, int32_t add_label_term, float *s_out,
                             float *grad_out, float *loss_out, void *workspace,
                             sg_stream_t stream, const sg_pair_source_t *src = nullptr,
-                            const int32_t *class_start = nullptr) {
+                            const int32_t *class_start = nullptr,
+                            const sg_adam_args_t *adam = nullptr) {
   if (n_pairs < 0 || pair_offset < 0) return SG_ERR_ARG;
   if (order && n_pairs > 0x7FFFFFFF) return SG_ERR_ARG;
   if (class_start && !order) return SG_ERR_ARG;
@@ -755,6 +826,7 @@ static int32_t fwd_bwd_impl(const sg_model_t *model, const void *records, const 
   hipStream_t st = (hipStream_t)stream;
   const int C = c.plan.n_params + 1;
   float *slab = (float *)workspace;
+  if (adam && n_pairs == 0) return SG_ERR_ARG;   // (no update from an empty batch)
   if (n_pairs == 0) {
     if (hipMemsetAsync(grad_out, 0, (size_t)c.plan.n_params * 4u, st) != hipSuccess)
       return SG_ERR_HIP;
@@ -762,12 +834,26 @@ static int32_t fwd_bwd_impl(const sg_model_t *model, const void *records, const 
     return SG_OK;
   }
   if (!records && !src) return SG_ERR_ARG;
+  // sg_train_step: the fused path's gradient reduction applies Adam in the same launch
+  // (sg_reduce_adam) with the step scalars the fused kernel's block 0 leaves in the
+  // reduction's partial rows (unused by the one-pass reduction)
+  const bool fuse_adam = adam && c.path == 1 && C - 1 <= 65536;
+  float *adam_pre = slab + ntn_offset_floats(c, n_pairs) - (int64_t)kReduceStrands * C;
+  SgAdamPre pre_args;
+  if (fuse_adam) {
+    pre_args.bp = adam->beta_powers;
+    pre_args.out = adam_pre;
+    pre_args.lr = adam->lr;
+    pre_args.b1 = adam->beta1;
+    pre_args.b2 = adam->beta2;
+    pre_args.wd = adam->weight_decay;
+  }
   int nblk = 0;
   int rc;
   if (c.path == 1)
     rc = sg_fast_run(model, c.plan, true, records, order, n_pairs, pair_offset, batch_total,
                      params, seed, y_stats, s_out, slab, slab + ntn_offset_floats(c, n_pairs),
-                     &nblk, st, seed_dev, src, class_start);
+                     &nblk, st, seed_dev, src, class_start, fuse_adam ? &pre_args : nullptr);
   else if (c.path == 2)
     rc = sg_fast32_run(model, c.plan, true, records, order, n_pairs, pair_offset, batch_total,
                        params, seed, y_stats, s_out, slab, slab + ntn_offset_floats(c, n_pairs),
@@ -776,9 +862,20 @@ static int32_t fwd_bwd_impl(const sg_model_t *model, const void *records, const 
     rc = sg_generic_run(c.plan, true, records, order, n_pairs, pair_offset, batch_total, params,
                         seed, y_stats, s_out, slab, &nblk, st);
   if (rc != SG_OK) return rc;
+  const int add_label = model->loss_mode == SG_LOSS_BROADCAST ? add_label_term : 0;
+  if (fuse_adam && nblk <= kOnePassRows) {
+    hipLaunchKernelGGL(sg_reduce_adam, dim3((C + 63) / 64), dim3(1024), 0, st, slab, nblk, C,
+                       grad_out, loss_out, y_stats, add_label, (float *)params, adam->m, adam->v,
+                       adam->beta1, adam->beta2, adam->eps, adam->weight_decay,
+                       (const float *)adam_pre, adam->beta_powers, adam->reg_loss_out);
+    return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
+  }
   float *part = slab + (size_t)nblk * C;
-  return launch_reduce(slab, nblk, C, part, grad_out, loss_out, y_stats,
-                       model->loss_mode == SG_LOSS_BROADCAST ? add_label_term : 0, st);
+  rc = launch_reduce(slab, nblk, C, part, grad_out, loss_out, y_stats, add_label, st);
+  if (rc != SG_OK || !adam) return rc;
+  return sg_adam_tf((float *)params, adam->m, adam->v, grad_out, C - 1, adam->lr, adam->beta1,
+                    adam->beta2, adam->eps, adam->weight_decay, adam->beta_powers,
+                    adam->reg_loss_out, stream);
 }
 
 int32_t sg_fwd_bwd_ex(const sg_model_t *model, const void *records, const int32_t *order,
@@ -800,6 +897,18 @@ int32_t sg_fwd_bwd_cls(const sg_model_t *model, const void *records, const int32
   return fwd_bwd_impl(model, records, order, n_pairs, pair_offset, batch_total, params, seed,
                       nullptr, y_stats, add_label_term, s_out, grad_out, loss_out, workspace,
                       stream, nullptr, class_start);
+}
+
+int32_t sg_train_step(const sg_model_t *model, const void *records, const int32_t *order,
+                      const int32_t *class_start, int64_t n_pairs, int64_t pair_offset,
+                      int64_t batch_total, float *params, uint64_t seed, const float *y_stats,
+                      int32_t add_label_term, float *s_out, float *grad_out, float *loss_out,
+                      void *workspace, const sg_adam_args_t *adam, sg_stream_t stream) {
+  if (!adam || !adam->m || !adam->v || !adam->beta_powers) return SG_ERR_ARG;
+  if (class_start && !order) return SG_ERR_ARG;
+  return fwd_bwd_impl(model, records, order, n_pairs, pair_offset, batch_total, params, seed,
+                      nullptr, y_stats, add_label_term, s_out, grad_out, loss_out, workspace,
+                      stream, nullptr, class_start, adam);
 }
 
 int32_t sg_fwd_bwd_src(const sg_model_t *model, const sg_pair_source_t *src,

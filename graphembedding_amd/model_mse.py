@@ -421,13 +421,33 @@ class SiameseGCNTNMSE(object):
                      self.beta1, self.beta2, self.eps, f.weight_decay, self.beta_powers,
                      self.reg_buf)
 
+    def fwd_bwd_adam(self, batch: Batch, seed=None, s_out=None, add_label_term=True):
+        """fwd_bwd + apply_adam as one library call (sg_train_step: on the fused path the
+        gradient reduction applies Adam in the same launch).  Same results as the two calls
+        (θ, m, v, grad, loss bitwise; reg_buf summed in another order).  Record batches
+        only; other batches take the two calls."""
+        if batch.csr is not None or batch.src is not None or self._adam_ws is not None:
+            self.fwd_bwd(batch, seed, s_out, add_label_term)
+            self.apply_adam()
+            return
+        f = self.flags
+        _lib.train_step(self.sg, batch.records, batch.n_pairs, batch.pair_offset,
+                        batch.batch_total, self.params, self._seed(seed), batch.y_stats,
+                        1 if add_label_term else 0, s_out, self.grad, self.loss_buf,
+                        self.workspace(batch.n_pairs), self.adam_m, self.adam_v,
+                        f.learning_rate, self.beta1, self.beta2, self.eps, f.weight_decay,
+                        self.beta_powers, self.reg_buf, order=batch.order,
+                        class_start=batch.cls)
+
     def train_step(self, batch: Batch, seed=None, sync=True):
         """sess.run([opt_op, loss]) (train.py:85,92): returns the loss evaluated
         at the pre-update parameters (incl. weight decay, models.py:67-88)."""
-        self.fwd_bwd(batch, seed)
-        if self.grad_hook is not None:
+        if self.grad_hook is None:
+            self.fwd_bwd_adam(batch, seed)
+        else:
+            self.fwd_bwd(batch, seed)
             self.grad_hook(self)
-        self.apply_adam()
+            self.apply_adam()
         self.step_count += 1
         if not sync:
             return None

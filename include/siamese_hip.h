@@ -407,6 +407,29 @@ int32_t sg_adam_tf_ex(float *params, float *m, float *v, const float *grad, int6
                       float *reg_loss_out, void *workspace, sg_stream_t stream);
 
 /*
+ * One training step (library 1.9): sg_fwd_bwd_cls (or sg_fwd_bwd_ex when class_start is
+ * NULL; order may then be NULL too) followed by sg_adam_tf on its gradient, i.e.
+ * sess.run([opt_op, loss]) (train.py:85,92) for one process.  On the fused path
+ * (sg_model_validate path 1) the gradient reduction applies the update in the same
+ * launch; other paths run the two calls.  params, grad_out, loss_out, m, v and
+ * beta_powers end as after sg_fwd_bwd_cls + sg_adam_tf, bitwise; reg_loss_out holds the
+ * same wd·½Σθ² summed in another order (double partials).  A multi-GPU step, whose
+ * gradient is all-reduced between the two, keeps the separate calls.  Replaces the
+ * train op of models.py:28-36 (AdamOptimizer(lr).minimize(loss)).
+ */
+typedef struct sg_adam_args {
+  float *m, *v;            /* device [n_params] moments */
+  float lr, beta1, beta2, eps, weight_decay;
+  float *beta_powers;      /* device [2] {β1^t, β2^t} (sg_adam_tf) */
+  float *reg_loss_out;     /* device [1] or NULL */
+} sg_adam_args_t;
+int32_t sg_train_step(const sg_model_t *model, const void *records, const int32_t *order,
+                      const int32_t *class_start, int64_t n_pairs, int64_t pair_offset,
+                      int64_t batch_total, float *params, uint64_t seed, const float *y_stats,
+                      int32_t add_label_term, float *s_out, float *grad_out, float *loss_out,
+                      void *workspace, const sg_adam_args_t *adam, sg_stream_t stream);
+
+/*
  * Pairs straight from the dense graph store (library 1.6).  sg_pack_pairs writes a
  * record per pair that the fused kernel then reads back: for a stream that does not
  * fit HBM at once (config C4, AIDS10knef all-pairs: 100.4 M pairs, 850 GB of

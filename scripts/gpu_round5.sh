@@ -6,7 +6,7 @@
 #   scripts/gpu_round5.sh TAG [skip-tests]    (variants: VARIANTS="ab/x.so ab/y.so",
 #                                              CLSW="1,1.315,1.316,1.493 ...",
 #                                              XCDW="10000,10000,... (8) ...",
-#                                              MODES="n1 emu8 c4 c5 c3 avg att")
+#                                              MODES="n1 emu8 n1ea emu8ea c4 c5 c3 avg att")
 set -u
 TAG=${1:-r05}
 SKIP=${2:-}
@@ -36,6 +36,10 @@ for rep in 1 2; do
     case $mode in
       n1) BENCH_ARGS_AB="--steps 40 --warmup 5" ;;
       emu8) BENCH_ARGS_AB="--emulate-world 8 --steps 300 --warmup 30" ;;
+      n1sep) BENCH_ARGS_AB="--steps 40 --warmup 5 --no-fused-adam" ;;
+      emu8sep) BENCH_ARGS_AB="--emulate-world 8 --steps 300 --warmup 30 --no-fused-adam" ;;
+      n1ea) BENCH_ARGS_AB="--steps 40 --warmup 5 --events after" ;;
+      emu8ea) BENCH_ARGS_AB="--emulate-world 8 --steps 300 --warmup 30 --events after" ;;
       c4) BENCH_ARGS_AB="--dataset syn_aids10knef --steps 2 --warmup 1" ;;
       c5) BENCH_ARGS_AB="--dataset syn_web --steps 3 --warmup 1" ;;
       c3) BENCH_ARGS_AB="--records bf16 --steps 40 --warmup 5" ;;
