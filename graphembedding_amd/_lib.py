@@ -144,6 +144,9 @@ def lib():
     L.sg_train_step.argtypes = [pm, vp, vp, vp, c_i64, c_i64, c_i64, vp, c_u64, vp, c_i32, vp,
                                 vp, vp, vp, ctypes.POINTER(SgAdamArgs), vp]
     L.sg_train_step.restype = c_i32
+    L.sg_train_step_dseed.argtypes = [pm, vp, vp, c_i64, c_i64, c_i64, vp, vp, vp, c_i32, vp,
+                                      vp, vp, vp, ctypes.POINTER(SgAdamArgs), vp]
+    L.sg_train_step_dseed.restype = c_i32
     L.sg_sampler_random.argtypes = [vp, vp, c_i32, c_i64, vp, vp]
     L.sg_sampler_random.restype = c_i32
     L.sg_sampler_density.argtypes = [vp, vp, vp, c_i32, c_i32, vp, c_i64, vp, vp]
@@ -197,7 +200,8 @@ EXPORTED_SYMBOLS = ('sg_version', 'sg_record_bytes', 'sg_record_bytes_ex', 'sg_m
                     'sg_web_workspace_bytes_ex', 'sg_web_release',
                     'sg_web_forward', 'sg_web_fwd_bwd', 'sg_fwd_bwd_dseed', 'sg_seed_advance',
                     'sg_feed_step', 'sg_pair_order_src', 'sg_forward_src', 'sg_fwd_bwd_src',
-                    'sg_pair_order_cls', 'sg_forward_cls', 'sg_fwd_bwd_cls', 'sg_train_step')
+                    'sg_pair_order_cls', 'sg_forward_cls', 'sg_fwd_bwd_cls', 'sg_train_step',
+                    'sg_train_step_dseed')
 
 # class_start entries of sg_pair_order_cls (include/siamese_hip.h SG_FAST_CLASSES_P1)
 FAST_CLASSES_P1 = 5
@@ -390,6 +394,20 @@ def train_step(m: SgModel, records, n_pairs, pair_offset, batch_total, params, s
                               int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(y_stats), int(add_label_term),
                               _ptr(s_out), _ptr(grad_out), _ptr(loss_out), _ptr(workspace),
                               ctypes.byref(a), _stream(stream)), 'sg_train_step')
+
+
+def train_step_dseed(m: SgModel, records, n_pairs, pair_offset, batch_total, params, seed_dev,
+                     y_stats, add_label_term, s_out, grad_out, loss_out, workspace, adam_m,
+                     adam_v, lr, beta1, beta2, eps, weight_decay, beta_powers, reg_loss=None,
+                     stream=None, order=None):
+    """sg_train_step_dseed: train_step with the dropout seed read from device memory."""
+    a = SgAdamArgs(_ptr(adam_m), _ptr(adam_v), float(lr), float(beta1), float(beta2), float(eps),
+                   float(weight_decay), _ptr(beta_powers), _ptr(reg_loss))
+    check(lib().sg_train_step_dseed(ctypes.byref(m), _ptr(records), _ptr(order), int(n_pairs),
+                                    int(pair_offset), int(batch_total), _ptr(params),
+                                    _ptr(seed_dev), _ptr(y_stats), int(add_label_term),
+                                    _ptr(s_out), _ptr(grad_out), _ptr(loss_out), _ptr(workspace),
+                                    ctypes.byref(a), _stream(stream)), 'sg_train_step_dseed')
 
 
 def fwd_bwd_dseed(m: SgModel, records, n_pairs, pair_offset, batch_total, params, seed_dev,

@@ -911,6 +911,18 @@ int32_t sg_train_step(const sg_model_t *model, const void *records, const int32_
                       stream, nullptr, class_start, adam);
 }
 
+int32_t sg_train_step_dseed(const sg_model_t *model, const void *records, const int32_t *order,
+                            int64_t n_pairs, int64_t pair_offset, int64_t batch_total,
+                            float *params, const uint64_t *seed_dev, const float *y_stats,
+                            int32_t add_label_term, float *s_out, float *grad_out,
+                            float *loss_out, void *workspace, const sg_adam_args_t *adam,
+                            sg_stream_t stream) {
+  if (!seed_dev || !adam || !adam->m || !adam->v || !adam->beta_powers) return SG_ERR_ARG;
+  return fwd_bwd_impl(model, records, order, n_pairs, pair_offset, batch_total, params, 0,
+                      seed_dev, y_stats, add_label_term, s_out, grad_out, loss_out, workspace,
+                      stream, nullptr, nullptr, adam);
+}
+
 int32_t sg_fwd_bwd_src(const sg_model_t *model, const sg_pair_source_t *src,
                        const int32_t *order, int64_t n_pairs, int64_t pair_offset,
                        int64_t batch_total, const float *params, uint64_t seed,

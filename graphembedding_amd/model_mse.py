@@ -546,9 +546,19 @@ class GraphSteps(object):
     def _body(self, ws):
         m = self.model
         b = self.feed.next_batch()
-        _lib.fwd_bwd_dseed(m.sg, b.records, b.n_pairs, b.pair_offset, b.batch_total, m.params,
-                           self.seed_dev, b.y_stats, 1, None, m.grad, m.loss_buf, ws)
-        m.apply_adam()
+        if m.grad_hook is None and m._adam_ws is None:   # reduction + Adam in one launch
+            f = m.flags
+            _lib.train_step_dseed(m.sg, b.records, b.n_pairs, b.pair_offset, b.batch_total,
+                                  m.params, self.seed_dev, b.y_stats, 1, None, m.grad,
+                                  m.loss_buf, ws, m.adam_m, m.adam_v, f.learning_rate, m.beta1,
+                                  m.beta2, m.eps, f.weight_decay, m.beta_powers, m.reg_buf)
+        else:
+            _lib.fwd_bwd_dseed(m.sg, b.records, b.n_pairs, b.pair_offset, b.batch_total,
+                               m.params, self.seed_dev, b.y_stats, 1, None, m.grad, m.loss_buf,
+                               ws)
+            if m.grad_hook is not None:
+                m.grad_hook(m)
+            m.apply_adam()
         _lib.seed_advance(self.seed_dev, 1)
 
     def _snapshot(self):

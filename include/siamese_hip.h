@@ -428,6 +428,14 @@ int32_t sg_train_step(const sg_model_t *model, const void *records, const int32_
                       int64_t batch_total, float *params, uint64_t seed, const float *y_stats,
                       int32_t add_label_term, float *s_out, float *grad_out, float *loss_out,
                       void *workspace, const sg_adam_args_t *adam, sg_stream_t stream);
+/* The same with the dropout seed read from device memory (sg_fwd_bwd_dseed): one
+ * hipGraph-captured reference step is feed → sg_train_step_dseed → sg_seed_advance. */
+int32_t sg_train_step_dseed(const sg_model_t *model, const void *records, const int32_t *order,
+                            int64_t n_pairs, int64_t pair_offset, int64_t batch_total,
+                            float *params, const uint64_t *seed_dev, const float *y_stats,
+                            int32_t add_label_term, float *s_out, float *grad_out,
+                            float *loss_out, void *workspace, const sg_adam_args_t *adam,
+                            sg_stream_t stream);
 
 /*
  * Pairs straight from the dense graph store (library 1.6).  sg_pack_pairs writes a
