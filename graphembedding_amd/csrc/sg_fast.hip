@@ -103,6 +103,7 @@ struct FastArgs {
   // slots are split over its waves in proportion to their XCD's weight when the waves hold
   // many pairs (SG_XCD_W)
   int xw[8];
+  int xw_even;   // all eight weights equal (the default): the split is plain integer shares
   int64_t n_pairs;
   int64_t pair_offset;
   int rw4h;      // 16-B words per HBM record (f32 or bf16 Â)
@@ -432,7 +433,19 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           // (8 positions per block, block b on XCD b % 8); the boundaries are integer
           // quotients of cumulative weights, so the shares tile the class exactly.
           const int q = nc / wc[c], r = nc - q * wc[c];
-          if (q >= 64) {
+          if (q >= 64 && A.xw_even) {
+            // equal weights: F(x) = w·x below, so the shares are floor(nc·k / wc) exactly;
+            // in 32 bits when nc·wc fits (a 64-bit division expands to a long scalar+VALU
+            // sequence on the prologue's critical path)
+            const int k = pos - cum;
+            if ((uint64_t)(uint32_t)nc * (uint32_t)wc[c] < (1ull << 32)) {
+              cs0 = cb[c] + (int)(((uint32_t)nc * (uint32_t)k) / (uint32_t)wc[c]);
+              cs1 = cb[c] + (int)(((uint32_t)nc * (uint32_t)(k + 1)) / (uint32_t)wc[c]);
+            } else {
+              cs0 = cb[c] + (int)((int64_t)nc * k / wc[c]);
+              cs1 = cb[c] + (int)((int64_t)nc * (k + 1) / wc[c]);
+            }
+          } else if (q >= 64) {
             auto F = [&](int x) -> int64_t {
               const int xb = (x >> 3) & 7;
               int64_t pre = 0, tot = 0;
@@ -1688,6 +1701,8 @@ static int fast_run_impl(const sg_model_t *m, const SgGenPlan &P, bool bwd, cons
     for (int k = 0; k < 4; ++k) A.cw[k] = 1.f;
     for (int k = 0; k < 8; ++k) A.xw[k] = 10000;
   }
+  A.xw_even = 1;
+  for (int k = 1; k < 8; ++k) A.xw_even &= A.xw[k] == A.xw[0] ? 1 : 0;
   A.n_pairs = n_pairs;
   A.rw4h = P.hbm_words / 4;
   A.rec_bf16 = P.adj_dtype == SG_DTYPE_BF16 ? 1 : 0;
