@@ -438,9 +438,13 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
             // in 32 bits when nc·wc fits (a 64-bit division expands to a long scalar+VALU
             // sequence on the prologue's critical path)
             const int k = pos - cum;
+            // (the 32-bit division expands on VALU: readfirstlane keeps the wave-uniform
+            // bounds in SGPRs, else the pair loop's slot tests become divergent branches)
             if ((uint64_t)(uint32_t)nc * (uint32_t)wc[c] < (1ull << 32)) {
-              cs0 = cb[c] + (int)(((uint32_t)nc * (uint32_t)k) / (uint32_t)wc[c]);
-              cs1 = cb[c] + (int)(((uint32_t)nc * (uint32_t)(k + 1)) / (uint32_t)wc[c]);
+              cs0 = cb[c] + __builtin_amdgcn_readfirstlane(
+                                (int)(((uint32_t)nc * (uint32_t)k) / (uint32_t)wc[c]));
+              cs1 = cb[c] + __builtin_amdgcn_readfirstlane(
+                                (int)(((uint32_t)nc * (uint32_t)(k + 1)) / (uint32_t)wc[c]));
             } else {
               cs0 = cb[c] + (int)((int64_t)nc * k / wc[c]);
               cs1 = cb[c] + (int)((int64_t)nc * (k + 1) / wc[c]);
