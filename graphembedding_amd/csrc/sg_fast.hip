@@ -760,6 +760,17 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
     N0 = N0 < 0 ? 0 : (N0 > D ? D : N0);
     N1 = N1 < 0 ? 0 : (N1 > D ? D : N1);
     const uint32_t pk = sg_pair_key(key, (uint32_t)(A.pair_offset + pcur));
+    // the hash inputs of layers 1 and 2 as (pk ^ lb) ^ element constant.  SG_HASH_OPAQUE = 1
+    // hides pk ^ lb from re-association (sg_fast32 does: there the per-lane invariants
+    // constant ^ lb, 24 of them, spilled to scratch); here it costs 2 VALU per pair and
+    // removes no spill (the 5 spilled values are reloaded before the pair loops only)
+#ifndef SG_HASH_OPAQUE
+#define SG_HASH_OPAQUE 0
+#endif
+    uint32_t pk1 = pk ^ lb1, pk2 = pk ^ lb2;
+#if SG_HASH_OPAQUE
+    asm("" : "+v"(pk1), "+v"(pk2));
+#endif
 
     // ---- layer-0 (node) and NTN-input dropout masks: one hash per lane, two ballots ----
     // lanes 0..15: layer 0, node e = l; lanes 16..31: layer 4, element e = l - 16.
@@ -837,7 +848,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           if (r < K0 || r < K1) {
-            const uint32_t h = sg_mix((pk ^ ((1u << 26) | (uint32_t)(128 * r + 16 * t))) ^ lb1);
+            const uint32_t h = sg_mix(pk1 ^ ((1u << 26) | (uint32_t)(128 * r + 16 * t)));
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
               float *T = sT + s * 16 * TS1 + (4 * g + r) * TS1 + 16 * t + j;
@@ -983,7 +994,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
         if (r < K0 || r < K1) {
-          const uint32_t h = sg_mix((pk ^ ((2u << 26) | (uint32_t)(64 * r))) ^ lb2);
+          const uint32_t h = sg_mix(pk2 ^ ((2u << 26) | (uint32_t)(64 * r)));
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
             if (r < (s ? K1 : K0)) {

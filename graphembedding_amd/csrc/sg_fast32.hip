@@ -438,6 +438,16 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
       };
       const uint32_t pk = sg_pair_key(A.key, (uint32_t)(A.pair_offset + p));
       const float label = sRec[L::TAIL + 2 * NC + 2];
+      // the hash inputs of layers 1 and 2 as (pk ^ lb) ^ element constant, with pk ^ lb
+      // opaque: re-associated as pk ^ (constant ^ lb), the 24 per-lane invariants were kept
+      // across the pair loop, spilled, and reloaded from scratch in every pair's hash loop
+      uint32_t pk1 = pk ^ lb1, pk2 = pk ^ lb2;
+#ifndef SG32_HASH_OPAQUE
+#define SG32_HASH_OPAQUE 1
+#endif
+#if SG32_HASH_OPAQUE
+      asm("" : "+v"(pk1), "+v"(pk2));
+#endif
 
       // ---- layer-0 (node) and NTN-input dropout masks: one hash per lane ----
       // lanes 0..31: layer 0, node e = l; lanes 32..63: layer 4, element e = l - 32
@@ -572,7 +582,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
           for (int f = 0; f < 2; ++f) {
             if (to < TM && nb < KBm) {
               const uint32_t h =
-                  sg_mix((pk ^ ((1u << 26) | (uint32_t)(512 * to + 128 * r + 16 * f))) ^ lb1);
+                  sg_mix(pk1 ^ ((1u << 26) | (uint32_t)(512 * to + 128 * r + 16 * f)));
   #pragma unroll
               for (int s = 0; s < 2; ++s) {
                 const uint32_t dr = s ? (h >> 16) : (h & 0xFFFFu);
@@ -635,7 +645,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
       for (int nb = 0; nb < 8; ++nb) {
         const int to = nb >> 2, r = nb & 3;
         if (to < TM && nb < KBm) {
-          const uint32_t h = sg_mix((pk ^ ((2u << 26) | (uint32_t)(256 * to + 64 * r))) ^ lb2);
+          const uint32_t h = sg_mix(pk2 ^ ((2u << 26) | (uint32_t)(256 * to + 64 * r)));
   #pragma unroll
           for (int s = 0; s < 2; ++s) {
             if (nb < (s ? KB1 : KB0)) {
