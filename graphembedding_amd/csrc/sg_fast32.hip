@@ -61,17 +61,20 @@ constexpr int MAXW = 8;    // waves per block (2 per SIMD)
 #ifndef SG32_NTN_KR
 #define SG32_NTN_KR 1
 #endif
+// the NTN V rows read ahead of the W products (1) or at use (0): C4 165.45 / 165.35 against
+// 163.83 / 163.85 M pairs/s (profiles/r05_z2, spill-free kernels)
 #ifndef SG32_V_HOIST
-#define SG32_V_HOIST 0
+#define SG32_V_HOIST 1
 #endif
 // gD1 = gZ1·W1ᵀ takes gZ1 with nodes on the lanes' rows (its A operand): SG32_GZ1T_LDS = 1
 // writes the gZ1 tiles (nodes on the accumulator rows) to the wave's D1 tile, free in the
 // backward, and reads them back transposed; 0 computes that orientation a second time on
 // the f32 MFMA (gH2ᵀ·Â: one MFMA per live k-block and tile).  Bitwise the same values.
 // Measured on C4 (profiles/r04_gz1t/c4): 152.1 / 152.3 against 152.3 / 152.2 M pairs/s
-// (the spills grow by 4 VGPRs), so the MFMA form stays the default here; sg_fast gains.
+// while the kernel spilled (the spills grew by 4 VGPRs); spill-free (SG32_HASH_OPAQUE)
+// 164.15 / 164.05 against 159.59 / 159.51 (profiles/r05_z): the LDS form is the default.
 #ifndef SG32_GZ1T_LDS
-#define SG32_GZ1T_LDS 0
+#define SG32_GZ1T_LDS 1
 #endif
 
 
