@@ -363,10 +363,6 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if args.events == 'after':
-        for _ in range(args.steps):
-            step(True)
-        torch.cuda.synchronize()
     params_agree = None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -382,6 +378,17 @@ def main():
         if not params_agree:
             print('bench.py: parameters differ across ranks after the timed steps',
                   file=sys.stderr, flush=True)
+    # the loss of the last timed step (before the event steps below move the parameters)
+    loss = float(model.loss_buf[0].item() + model.reg_buf[0].item())
+    event_steps = 0
+    if args.events == 'after':
+        # the roofline's kernel time: HIP events around as many extra training steps right
+        # after the timed region (they keep training: params, Adam state and step_count
+        # advance by event_steps more; params_agree and loss above are the timed run's)
+        for _ in range(args.steps):
+            step(True)
+        torch.cuda.synchronize()
+        event_steps = args.steps
 
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     total_pairs = shard.total
@@ -398,7 +405,6 @@ def main():
     value = total_pairs * args.steps / elapsed
     if ew:
         value = shard.n * args.steps / elapsed   # diagnostic: one emulated rank's own rate
-    loss = float(model.loss_buf[0].item() + model.reg_buf[0].item())
 
     if rank == 0:
         flops_pair = gs.flops_per_pair_web() if web else gs.flops_per_pair(
@@ -525,6 +531,7 @@ def main():
             'cpu_baseline': cpu,
             'forward_pairs_per_s': fwd_rate,
             'loss': loss,
+            'event_steps_after_timed': event_steps,
             'params_agree_across_ranks': params_agree,
         }
         line = json.dumps(out)

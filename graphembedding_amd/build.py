@@ -57,7 +57,7 @@ SOURCE_FLAGS = {'sg_fast.hip': ['-mllvm', '-amdgpu-sched-strategy=max-ilp'],
 
 
 def build_hip(force: bool = False, verbose: bool = False, out: str = None, defines=()) -> str:
-    """Build the library in-tree; `out`/`defines` build an A/B variant (e.g. SG_FAST_MAXW=8).
+    """Build the library in-tree; `out`/`defines` build an A/B variant (e.g. -DSG_FAST_TIMING=1).
     Each source compiles to its own object (in parallel), then one link."""
     if out is None and not force and not _stale():
         return OUT

@@ -11,19 +11,11 @@
 // compile only together with SG_TIMING_ABLATION_BUILD, which build.py never passes to
 // the product library (graphembedding_amd/lib/libsiamese_hip.so), so a hand build
 // with one ablation macro alone fails here instead of producing a silently wrong .so.
-#if (defined(SG32_ABL_NOREC) || defined(SG32_ABL_NONTN) || defined(SG_WEB_ABL_NOH2) || \
-     defined(SG_WEB_ABL_FHASH) || defined(SG_WEB_ABL_FH1) || defined(SG_WEB_ABL_FH2)) && \
+#if (defined(SG32_ABL_NOREC) || defined(SG32_ABL_NONTN) || defined(SG_WEB_ABL_NOH2)) && \
     !defined(SG_TIMING_ABLATION_BUILD)
 #error "timing ablation macro without SG_TIMING_ABLATION_BUILD: results would be invalid"
 #endif
 
-// ---------------------------------------------------------------------------
-// Counter-based dropout RNG.  Bit-exact twin of oracle/siamese_oracle.py
-// (sg_mix, seed_key, dropout_mask).  Replaces TF's unseeded
-// floor(keep + U[0,1)) masks of layers.py:332-338 / tf.nn.dropout.
-// ---------------------------------------------------------------------------
-// 24-bit-multiply lowbias32 variant: (x & 0xFFFFFF) * C is one full-rate
-// v_mul_u32_u24 on gfx950.
 // sg_train_step: what the fused kernel's block 0 needs to compute ApplyAdam's step
 // scalars out[4] = {α, β1^t·β1, β2^t·β2, wd·½Σθ²} before the reduction launch applies the
 // update (host struct, copied into the kernel arguments)
@@ -33,6 +25,13 @@ struct SgAdamPre {
   float lr, b1, b2, wd;
 };
 
+// ---------------------------------------------------------------------------
+// Counter-based dropout RNG.  Bit-exact twin of oracle/siamese_oracle.py
+// (sg_mix, seed_key, dropout_mask).  Replaces TF's unseeded
+// floor(keep + U[0,1)) masks of layers.py:332-338 / tf.nn.dropout.
+// ---------------------------------------------------------------------------
+// 24-bit-multiply lowbias32 variant: (x & 0xFFFFFF) * C is one full-rate
+// v_mul_u32_u24 on gfx950.
 __host__ __device__ __forceinline__ uint32_t sg_mix(uint32_t x) {
   x ^= x >> 16;
   x = (x & 0xFFFFFFu) * 0x7FEB35u;

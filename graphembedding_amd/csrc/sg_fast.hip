@@ -41,53 +41,21 @@ constexpr int TS1 = 36;  // D1 tile row stride (floats)
 constexpr int TS2 = 20;  // gZ1 tile row stride
 constexpr int W1S = 20;  // W1 table row stride (16 + pad)
 constexpr int W1TS = 36; // W1ᵀ table row stride (32 + pad)
-// gD1 = gZ1·W1ᵀ on bf16 MFMA with both operands split in three parts (x = h + m + l,
-// the six leading products: ≈ f32 accuracy); W1's parts are built once per launch
-#ifndef SG_GD1_BF16
-#define SG_GD1_BF16 1
-#endif
-// Scheduling fences around each f32 MFMA product (SG_MFMA_CLUSTER = 1: all but gZ0,
-// 2: all): its MFMAs then issue back to back instead of one at a time between VALU
-// instructions.  On gfx950 every switch between v_mfma_f32_16x16x4_f32 and VALU in a
-// wave's stream costs issue cycles (scripts/mfma_valu_mix.hip: 4 MFMAs + 48 FMAs take
-// 7.6% longer interleaved than grouped); the scheduler's default is to interleave.
-// Measured 470.3 -> 480.7 M pairs/s (level 2); fencing the bf16 gD1 MFMAs too: 477.3.
-#ifndef SG_MFMA_CLUSTER
-#define SG_MFMA_CLUSTER 2
-#endif
-#if SG_MFMA_CLUSTER
-#define SG_CLUSTER() __builtin_amdgcn_sched_barrier(0)
-#else
-#define SG_CLUSTER() do {} while (0)
-#endif
-#if SG_MFMA_CLUSTER >= 2
-#define SG_CLUSTER2() __builtin_amdgcn_sched_barrier(0)
-#else
-#define SG_CLUSTER2() do {} while (0)
-#endif
-#ifndef SG_FAST_MAXW
-#define SG_FAST_MAXW 8
-#endif
-// gD1 = gZ1·W1ᵀ takes gZ1 with nodes on the lanes' rows (its A operand): SG_GZ1T_LDS = 1
-// writes the gZ1 tile (nodes on the accumulator rows, as Âᵀ·gH2 leaves it) to the wave's
-// LDS and reads it back transposed; 0 computes that orientation a second time on the f32
-// MFMA (gH2ᵀ·Â, 2-3 MFMAs per side, 4 for a shared tile).  The values are bitwise the
-// same (Â is symmetric and both products sum over the same nodes in the same order).
-#ifndef SG_GZ1T_LDS
-#define SG_GZ1T_LDS 1
-#endif
+// gD1 = gZ1·W1ᵀ runs on bf16 MFMA with both operands split in three parts (x = h + m + l,
+// the six leading products: ≈ f32 accuracy); W1's parts are built once per launch.  It
+// takes gZ1 with nodes on the lanes' rows (its A operand): the gZ1 tile (nodes on the
+// accumulator rows, as Âᵀ·gH2 leaves it) goes through the wave's LDS and is read back
+// transposed.  (The variants these replaced, and their measurements, are in
+// profiles/HISTORY.md: f32 gD1, gZ1ᵀ recomputed on the f32 MFMA.)
+//
+// Scheduling fence around each f32 MFMA product: its MFMAs then issue back to back instead
+// of one at a time between VALU instructions.  On gfx950 every switch between
+// v_mfma_f32_16x16x4_f32 and VALU in a wave's stream costs issue cycles
+// (scripts/mfma_valu_mix.hip: 4 MFMAs + 48 FMAs take 7.6% longer interleaved than grouped);
+// the scheduler's default is to interleave.  Measured 470.3 -> 480.7 M pairs/s.
+__device__ __forceinline__ void mfma_fence() { __builtin_amdgcn_sched_barrier(0); }
 // waves per block: 8 = 2 waves per SIMD at up to 256 VGPRs per lane
-constexpr int MAXW = SG_FAST_MAXW;
-// class-exclusive schedule: the waves that take one pair more than the others in their
-// class are the older waves of their SIMD pairs (1), or spread by the even split (0)
-#ifndef SG_LONG_OLD
-#define SG_LONG_OLD 1
-#endif
-// ... and the two waves of a SIMD take the same class (1), or the classes are contiguous
-// ranges of the grid's wave index (0)
-#ifndef SG_PAIR_ALIGN
-#define SG_PAIR_ALIGN 1
-#endif
+constexpr int MAXW = 8;
 
 struct FastArgs {
   const uint8_t *recs;
@@ -205,15 +173,15 @@ struct FastLds {
   static constexpr int GE = X + 48;                   // AVG: ∂L/∂x1 | ∂L/∂x2 (16 each)
   static constexpr int TMP = GE + 32;                 // ATT: node means of H2 (16 per side)
   static constexpr int GU = TMP + 32;                 // ATT: ∂L/∂(tanh input) (16 per side)
-  static constexpr int GT = GU + 32;                  // SG_GZ1T_LDS: gZ1 tiles, 2 x 16 x TS2
+  static constexpr int GT = GU + 32;                  // gZ1 tiles, 2 x 16 x TS2
   // (the gZ1 tiles only in the backward: the forward-only kernel keeps its smaller
   // regions and with them two blocks per CU)
   static int wave_floats(int, bool bwd) {
-    return (SG_GZ1T_LDS && bwd) ? GT + 2 * 16 * TS2 : X + 48 + (AVG ? 32 : 0) + (ATT ? 64 : 0);
+    return bwd ? GT + 2 * 16 * TS2 : X + 48 + (AVG ? 32 : 0) + (ATT ? 64 : 0);
   }
   static int shared_floats(int d_in) {
     return (d_in + 1) * FH1 + 2 * DN * FK * WR + FK * VS + FH1 * W1S + FH2 * W1TS +
-           (SG_GD1_BF16 ? 2 * 3 * 64 * 4 : 0) + (ATT ? FH2 * WAS : 0);
+           2 * 3 * 64 * 4 + (ATT ? FH2 * WAS : 0);
   }
 };
 
@@ -267,20 +235,10 @@ __device__ __forceinline__ int fast_param(const FastArgs &A, int s, int l) {
   return (ATT && s < 4) ? A.oWa + (4 * s + g) * FH2 + j : -1;
 }
 
-// The NTN head's FMAs over element pairs (b, b + 1): one v_pk_fma_f32 (SG_NTN_PK = 1) or
-// two v_fma_f32 (0); the same two fmaf chains either way, so the results are bitwise equal.
-// Unlike split3's packed subtractions (SG_SPLIT_PK), these keep their register pairs: the
-// plain form measured 1.1% slower on C2 and 0.7% at an emulated W = 8 rank (profiles/r05_n).
-#ifndef SG_NTN_PK
-#define SG_NTN_PK 1
-#endif
-__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) {
-#if SG_NTN_PK
-  return __builtin_elementwise_fma(a, b, c);
-#else
-  return f2{fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y)};
-#endif
-}
+// The NTN head's FMAs over element pairs (b, b + 1): one v_pk_fma_f32, the same two fmaf
+// chains as two v_fma_f32.  Unlike split3's packed subtractions (SG_SPLIT_PK), these keep
+// their register pairs: the plain form measured 1.1% slower on C2 (profiles/r05_n).
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 // tanh and the logistic function from v_exp_f32 and v_rcp_f32 (the Attention layer's h
 // and att, layers.py:156-157).  Both are ≈1e-7 ABSOLUTE error: sg_tanh's 1 - 2/(e^2z + 1)
@@ -384,11 +342,11 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       tot += wt[c];
       nonempty += nc > 0;
     }
-    // SG_PAIR_ALIGN: the two waves of a SIMD (w and w ^ 4 of a block) always take the same
-    // class: the waves are allocated in SIMD pairs and enumerated block by block in the order
+    // the two waves of a SIMD (w and w ^ 4 of a block) always take the same class: the
+    // waves are allocated in SIMD pairs and enumerated block by block in the order
     // (0, 4, 1, 5, 2, 6, 3, 7), so no SIMD runs pairs of two classes side by side (two
     // classes' pair costs were fitted with partners of their own class)
-    const bool align = SG_PAIR_ALIGN && nw == 8;
+    const bool align = nw == 8;
     const int units = align ? stride >> 1 : stride;
     const int pos = align ? (gw & ~7) + 2 * (gw & 3) + ((gw >> 2) & 1) : gw;
     if (nonempty > 0 && units >= nonempty) {
@@ -424,7 +382,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         if (cwave < 0 && pos < cum + wc[c]) {
           const int nc = cb[c + 1] - cb[c];
           cwave = c;
-#if SG_LONG_OLD
           // A class's nc slots over its wc waves.  Waves holding many pairs (N = 1 sizes)
           // split them in proportion to their XCD's weight: the XCDs run the pair loop at
           // measurably different speeds, the same on every box measured (profiles/r05_f,
@@ -483,11 +440,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
             cs0 = cb[c] + k * q + min(k, r);
             cs1 = cs0 + q + (k < r ? 1 : 0);
           }
-#else
-          const int k = pos - cum;
-          cs0 = cb[c] + (int)((int64_t)k * nc / wc[c]);
-          cs1 = cb[c] + (int)((int64_t)(k + 1) * nc / wc[c]);
-#endif
         }
         cum += wc[c];
       }
@@ -521,11 +473,11 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   float *sV = sWb + DN * FK * WR;               // [k][VS]
   float *sW1 = sV + FK * VS;                    // W1 · ik1 [32][16], row stride W1S (gD1)
   float *sW1T = sW1 + FH1 * W1S;                // W1ᵀ [16][32], row stride W1TS (Z1)
-  // [t][term][lane] bf16 B operands of gD1 (SG_GD1_BF16): lane (g, j) ↔ column 16t + j,
+  // [t][term][lane] bf16 B operands of gD1: lane (g, j) ↔ column 16t + j,
   // k-slots 8g..8g+3 / 8g+4..8g+7 ↔ parts of W1[16t + j][4g..4g+3]·ik1
   uint4 *sW1B = (uint4 *)(sW1T + FH2 * W1TS);
   // ATT: Attention weights Wa[j'][k] at row stride WAS
-  float *sWat = SG_GD1_BF16 ? (float *)(sW1B + 2 * 3 * 64) : sW1T + FH2 * W1TS;
+  float *sWat = (float *)(sW1B + 2 * 3 * 64);
   float *W = smem + A.shared_floats + wv * A.wave_floats;
   float *sRec = W + L::REC;
   float *sT = W + L::TILE;
@@ -590,7 +542,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
     sW1[(i / FH2) * W1S + i % FH2] = w * A.ik1;
     sW1T[(i % FH2) * W1TS + i / FH2] = w;
   }
-#if SG_GD1_BF16
   for (int i = tid; i < 2 * 3 * 64; i += blockDim.x) {
     const int t = i / 192, term = (i / 64) % 3, ln = i & 63;
     const int f = 16 * t + (ln & 15), k0 = 4 * (ln >> 4);
@@ -601,7 +552,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
     sW1B[i] = term == 0 ? uint4{h01, h23, h01, h23}
                         : (term == 1 ? uint4{m01, m23, h01, h23} : uint4{l01, l23, m01, m23});
   }
-#endif
   if constexpr (ATT)
     for (int i = tid; i < FH2 * FH2; i += blockDim.x) sWat[(i >> 4) * WAS + (i & 15)] = stg[A.oWa + i];
   // per-lane parameters, also from the staged copy
@@ -626,10 +576,8 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   SG_STAMP(1, __builtin_amdgcn_s_memrealtime());
 
   // ---- per-lane constants ----
-  // MFMA B fragments of W1 read from LDS at use: W1[8g+q][j] (Z1 = D1 W1) and
-  // ik1 · W1[16t+j][4g+q] (gD1 = gZ1 W1ᵀ), contiguous in their tables
+  // MFMA B fragment of W1 read from LDS at use: W1[8g+q][j] (Z1 = D1 W1)
   const float *w1bp = sW1T + j * W1TS + 8 * g;
-  const float *w1tp = sW1 + j * W1S + 4 * g;
   // NTN lane role: k = j (valid < FK); rows a = 4r + g, r < 3 (valid < D)
   // A-operand row of this lane: tile row i = j ↔ node ni.  Â is read at static
   // per-lane offsets; entries outside the n_max × n_max block (tile rows and
@@ -649,12 +597,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   // side 1's row i - 2.  This lane's A row i = j comes from side jp, row jr.
   const int jp = (j >> 1) & 1, jr = j - 2 * jp;
   const float *sTp = sT + jp * 16 * TS1 + jr * TS1 + 8 * g;   // shared-tile D1 row j
-  int afp[2];   // side 1's Â row ni(j-2) on lanes jp = 1, zero elsewhere (B of the shared gZ1ᵀ)
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int nr = 4 * (jr & 3) + (jr >> 2), c = 4 * q + g;
-    afp[q] = (jp && nr < D && c < D) ? L::REC + D * D + nr * D + c : L::X + 47;
-  }
   int tyo[3];   // record word of the type of node 4r + g (side 0; side 1 at + D)
 #pragma unroll
   for (int r = 0; r < 3; ++r) tyo[r] = 2 * D * D + (4 * r + g < D ? 4 * r + g : 0);
@@ -683,15 +625,10 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   // Waves w and w ^ 4 share a SIMD (round-robin placement).  Issue arbitration
   // favours the older wave, which would finish its pairs far ahead and leave the
   // younger one alone on the SIMD for the last ~third of the launch.  The higher
-  // priority alternates between the two by pair count (SG_PRIO_PERIOD pairs, the
-  // younger wave holding it in SG_PRIO_YOUNG of them); ties still favour the
+  // priority alternates between the two by pair count (PRIO_PERIOD pairs, the
+  // younger wave holding it in PRIO_YOUNG of them); ties still favour the
   // older wave.  The pair → wave assignment is unchanged.
-#ifndef SG_PRIO_PERIOD
-#define SG_PRIO_PERIOD 3
-#endif
-#ifndef SG_PRIO_YOUNG
-#define SG_PRIO_YOUNG 2
-#endif
+  constexpr int PRIO_PERIOD = 3, PRIO_YOUNG = 2;
   int it = 0;
   const int young = wv >> 2;   // 0 / 1, wave-uniform (scalar)
   // The pair loop: CLS < 0 = mixed schedule (each pair dispatches to its (K0, K1) body);
@@ -702,7 +639,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
   for (; q < qend; ++it) {
     // (scalar integers: as bools the comparison went through VALU selects; one
     // conditional instead of an if / else)
-    const int yturn = (int)((unsigned)((it % SG_PRIO_PERIOD) - SG_PRIO_YOUNG) >> 31);   // < YOUNG
+    const int yturn = (int)((unsigned)((it % PRIO_PERIOD) - PRIO_YOUNG) >> 31);   // < YOUNG
     __builtin_amdgcn_s_setprio(0);
     if ((yturn ^ young) == 0) __builtin_amdgcn_s_setprio(1);
     sg_wsync();
@@ -760,17 +697,9 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
     N0 = N0 < 0 ? 0 : (N0 > D ? D : N0);
     N1 = N1 < 0 ? 0 : (N1 > D ? D : N1);
     const uint32_t pk = sg_pair_key(key, (uint32_t)(A.pair_offset + pcur));
-    // the hash inputs of layers 1 and 2 as (pk ^ lb) ^ element constant.  SG_HASH_OPAQUE = 1
-    // hides pk ^ lb from re-association (sg_fast32 does: there the per-lane invariants
-    // constant ^ lb, 24 of them, spilled to scratch); here it costs 2 VALU per pair and
-    // removes no spill (the 5 spilled values are reloaded before the pair loops only)
-#ifndef SG_HASH_OPAQUE
-#define SG_HASH_OPAQUE 0
-#endif
-    uint32_t pk1 = pk ^ lb1, pk2 = pk ^ lb2;
-#if SG_HASH_OPAQUE
-    asm("" : "+v"(pk1), "+v"(pk2));
-#endif
+    // the hash inputs of layers 1 and 2 as (pk ^ lb) ^ element constant (sg_fast32 hides
+    // pk ^ lb from re-association against spills; here that measured 1.2% slower)
+    const uint32_t pk1 = pk ^ lb1, pk2 = pk ^ lb2;
 
     // ---- layer-0 (node) and NTN-input dropout masks: one hash per lane, two ballots ----
     // lanes 0..15: layer 0, node e = l; lanes 16..31: layer 4, element e = l - 16.
@@ -830,7 +759,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           }
         }
         tys[s] = tp;
-        SG_CLUSTER();
+        mfma_fence();
 #pragma unroll
         for (int t = 0; t < 2; ++t) {   // ik1 · P1 = Â Z0 + ik1 b0  (absent rows: ik1 b0, never read)
           const float bb = t ? b0v1 : b0v0;
@@ -839,7 +768,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           for (int q = 0; q < KS; ++q) acc = mfma4(af[s][q], z0[t][q], acc);
           p1[s][t] = acc;
         }
-        SG_CLUSTER();
+        mfma_fence();
       }
       // D1 = dropout(ik1 relu(P1)): one hash per element (node 4r+g, feature
       // 16t+j) gives both sides' draws.  The backward reads keep·relu' back as D1 > 0.
@@ -873,7 +802,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         const f4 lo = *(const f4 *)sTp, hi = *(const f4 *)(sTp + 4);
         const f4 wlo = *(const f4 *)w1bp, whi = *(const f4 *)(w1bp + 4);
         f4 z1 = {0.f, 0.f, 0.f, 0.f};
-        SG_CLUSTER();
+        mfma_fence();
 #pragma unroll
         for (int q = 0; q < 4; ++q) z1 = mfma4(lo[q], wlo[q], z1);
 #pragma unroll
@@ -885,7 +814,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           acc = mfma4(af[s][1], z1[2 * s + 1], acc);
           h2[s] = acc;
         }
-        SG_CLUSTER();
+        mfma_fence();
       } else {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {   // Z1 = D1 W1 ; H2 = Â Z1 + b1
@@ -894,7 +823,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           const f4 lo = *(const f4 *)T, hi = *(const f4 *)(T + 4);
           const f4 wlo = *(const f4 *)w1bp, whi = *(const f4 *)(w1bp + 4);
           f4 z1 = {0.f, 0.f, 0.f, 0.f};
-          SG_CLUSTER();
+          mfma_fence();
 #pragma unroll
           for (int q = 0; q < 4; ++q) z1 = mfma4(lo[q], wlo[q], z1);
 #pragma unroll
@@ -903,7 +832,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
 #pragma unroll
           for (int q = 0; q < KS; ++q) acc = mfma4(af[s][q], z1[q], acc);
           h2[s] = acc;
-          SG_CLUSTER();
+          mfma_fence();
         }
       }
       // D2 = dropout(H2) (one hash per element, both sides); zpre = D2·Wd + bd;
@@ -1244,48 +1173,28 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int q = 0; q < KS; ++q) dq[s][t][q] = T1[q * TS1 + 16 * t];
-        SG_CLUSTER();
+        mfma_fence();
 #pragma unroll
         for (int q = 0; q < KS; ++q) {
           gz1 = mfma4(af[s][q], gh2[s][q], gz1);
-          if (!PACK && !SG_GZ1T_LDS) gz1t[s] = mfma4(gh2[s][q], af[s][q], gz1t[s]);
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int q = 0; q < KS; ++q) gw1[t] = mfma4(dq[s][t][q], gz1[q], gw1[t]);
-        SG_CLUSTER();
-#if SG_GZ1T_LDS
+        mfma_fence();
         {   // gZ1 rows 4g + r, feature j (a shared tile: side 1's rows 2 below side 0's)
           float *gt = W + L::GT + (PACK ? 0 : s * 16 * TS2) + j;
 #pragma unroll
           for (int r = 0; r < KS; ++r) gt[(4 * g + r + ((PACK && s) ? 2 : 0)) * TS2] = gz1[r];
         }
-#endif
       }
-#if SG_GZ1T_LDS
       sg_wsync();
 #pragma unroll
       for (int s = 0; s < (PACK ? 1 : 2); ++s)
         gz1t[s] = *(const f4 *)(W + L::GT + s * 16 * TS2 + j * TS2 + 4 * g);
-#else
-      if constexpr (PACK) {
-        // gZ1ᵀ of both sides in the shared layout: side 0's Â rows are zero on the
-        // lanes of side 1's rows (nodes >= 8 are absent), afp holds side 1's rows there
-        f4 c = {0.f, 0.f, 0.f, 0.f};
-        const float afp0 = W[afp[0]], afp1 = W[afp[1]];
-        SG_CLUSTER();
-        c = mfma4(gh2[0][0], af[0][0], c);
-        c = mfma4(gh2[0][1], af[0][1], c);
-        c = mfma4(gh2[1][0], afp0, c);
-        c = mfma4(gh2[1][1], afp1, c);
-        gz1t[0] = c;
-        SG_CLUSTER();
-      }
-#endif
       // gD1 · ik1 = gZ1 (W1 ik1)ᵀ per feature tile t (one chain per tile when packed)
       f4 gd[2][2];   // [side, or 0 = shared][t]
-#if SG_GD1_BF16
       // A k-slots 8g..8g+7 = (h | m) or (h | l) of gZ1[i][4g..4g+3]; with the B parts
       // (Wh | Wh), (Wm | Wh), (Wl | Wm): hh + mh + hm + lh + hl + mm in three MFMAs
       uint4 ahm[2], ahl[2];
@@ -1310,19 +1219,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           gd[s][t] = acc;
         }
       }
-#else
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const f4 wt = *(const f4 *)(w1tp + 16 * t * W1S);
-#pragma unroll
-        for (int s = 0; s < (PACK ? 1 : 2); ++s) {
-          f4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int q = 0; q < 4; ++q) acc = mfma4(gz1t[s][q], wt[q], acc);
-          gd[s][t] = acc;
-        }
-      }
-#endif
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int KS = s ? K1 : K0;
@@ -1359,10 +1255,10 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           if (t) gb0a1 += (gp1[0] + gp1[1]) + gp1[2];
           else gb0a0 += (gp1[0] + gp1[1]) + gp1[2];
           f4 gz0 = {0.f, 0.f, 0.f, 0.f};  // gZ0 = Âᵀ gP1
-          SG_CLUSTER2();
+          mfma_fence();
 #pragma unroll
           for (int q = 0; q < KS; ++q) gz0 = mfma4(af[s][q], gp1[q], gz0);
-          SG_CLUSTER2();
+          mfma_fence();
           // gW0 / ik0 += Xᵀ gZ0 (rows 4g+3 of gZ0 are always zero)
           uint32_t h01, m01, l01, h23 = 0u, m23 = 0u, l23 = 0u;
           split3(gz0[0], gz0[1], h01, m01, l01);

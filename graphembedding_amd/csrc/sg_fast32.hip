@@ -52,30 +52,12 @@ __device__ __forceinline__ int wa_swz(int k, int a) {
 constexpr int VS = 66;
 constexpr int NBUF = 80;   // NTN buffer floats per pair: x1[32] | x2[32] | gm[16]
 constexpr int MAXW = 8;    // waves per block (2 per SIMD)
-#ifndef SG32_HOIST_P1
-#define SG32_HOIST_P1 1
-#endif
-#ifndef SG32_AF_ALL
-#define SG32_AF_ALL 1
-#endif
-#ifndef SG32_NTN_KR
-#define SG32_NTN_KR 1
-#endif
-// the NTN V rows read ahead of the W products (1) or at use (0): C4 165.45 / 165.35 against
-// 163.83 / 163.85 M pairs/s (profiles/r05_z2, spill-free kernels)
-#ifndef SG32_V_HOIST
-#define SG32_V_HOIST 1
-#endif
-// gD1 = gZ1·W1ᵀ takes gZ1 with nodes on the lanes' rows (its A operand): SG32_GZ1T_LDS = 1
-// writes the gZ1 tiles (nodes on the accumulator rows) to the wave's D1 tile, free in the
-// backward, and reads them back transposed; 0 computes that orientation a second time on
-// the f32 MFMA (gH2ᵀ·Â: one MFMA per live k-block and tile).  Bitwise the same values.
-// Measured on C4 (profiles/r04_gz1t/c4): 152.1 / 152.3 against 152.3 / 152.2 M pairs/s
-// while the kernel spilled (the spills grew by 4 VGPRs); spill-free (SG32_HASH_OPAQUE)
-// 164.15 / 164.05 against 159.59 / 159.51 (profiles/r05_z): the LDS form is the default.
-#ifndef SG32_GZ1T_LDS
-#define SG32_GZ1T_LDS 1
-#endif
+// The NTN V rows are read ahead of the W products (C4 165.45 / 165.35 against 163.83 /
+// 163.85 M pairs/s read at use, profiles/r05_z2).  gD1 = gZ1·W1ᵀ takes gZ1 with nodes on
+// the lanes' rows (its A operand): the gZ1 tiles (nodes on the accumulator rows) go through
+// the wave's D1 tile, free in the backward, and are read back transposed (164.15 / 164.05
+// against 159.59 / 159.51 recomputing that orientation on the f32 MFMA, profiles/r05_z).
+// The losing variants of these and the other round-4/5 A/Bs are in profiles/HISTORY.md.
 
 
 struct F32Args {
@@ -301,18 +283,12 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
 
   // wave priority as sg_fast: waves w and w ^ 4 share a SIMD; the higher priority
   // alternates between them by pair count so that neither finishes far ahead
-#ifndef SG_PRIO32_PERIOD
-#define SG_PRIO32_PERIOD 3
-#endif
-#ifndef SG_PRIO32_YOUNG
-#define SG_PRIO32_YOUNG 2
-#endif
   const int young = wv >> 2;   // 0 / 1, wave-uniform (scalar)
   for (int it = 0;; ++it) {
     const int q = slot_of(it);
     if (q >= npairs) break;
-    if (SG_PRIO32_PERIOD > 0) {
-      const int yturn = (int)((unsigned)((it % SG_PRIO32_PERIOD) - SG_PRIO32_YOUNG) >> 31);
+    {   // period 3 pairs, the younger wave first in 2 of them
+      const int yturn = (int)((unsigned)((it % 3) - 2) >> 31);
       __builtin_amdgcn_s_setprio(0);   // (scalar, one conditional, as sg_fast)
       if ((yturn ^ young) == 0) __builtin_amdgcn_s_setprio(1);
     }
@@ -445,12 +421,7 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
       // opaque: re-associated as pk ^ (constant ^ lb), the 24 per-lane invariants were kept
       // across the pair loop, spilled, and reloaded from scratch in every pair's hash loop
       uint32_t pk1 = pk ^ lb1, pk2 = pk ^ lb2;
-#ifndef SG32_HASH_OPAQUE
-#define SG32_HASH_OPAQUE 1
-#endif
-#if SG32_HASH_OPAQUE
       asm("" : "+v"(pk1), "+v"(pk2));
-#endif
 
       // ---- layer-0 (node) and NTN-input dropout masks: one hash per lane ----
       // lanes 0..31: layer 0, node e = l; lanes 32..63: layer 4, element e = l - 32
@@ -479,13 +450,8 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
           const int ab = abase0 + s * NC * RS + 4 * b;
           // unconditional: entries past N are zero (record contract), and reads without a
           // per-k-block branch issue together (one LDS round trip instead of one per block)
-  #if SG32_AF_ALL
           af[0][b] = b < 4 * T ? W[ab] : 0.f;
           af[1][b] = T > 1 ? W[ab + 16 * RS] : 0.f;
-  #else
-          af[0][b] = b < KB ? W[ab] : 0.f;
-          af[1][b] = (b < KB && T > 1) ? W[ab + 16 * RS] : 0.f;
-  #endif
         }
       };
 
@@ -502,7 +468,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
           d1[s][to][0] = f4{b0v0, b0v0, b0v0, b0v0};
           d1[s][to][1] = f4{b0v1, b0v1, b0v1, b0v1};
         }
-  #if SG32_HOIST_P1
         // types, W0 rows and Â fragments of all eight k-blocks first (unconditional reads,
         // two dependent LDS round trips per side instead of two per k-block): nodes past N
         // are masked (k0 = 0 -> the zero row d_in), Â is zero there
@@ -546,31 +511,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
             }
           }
         }
-  #else
-  #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-          if (kb_live(b, T, KB)) {
-            const int n = 4 * b + g;
-            uint32_t t_ = (uint32_t)ty[s * NC + n];
-            t_ = min(t_, (uint32_t)(d_in - 1));
-            const uint32_t k0 = (kms >> n) & 1u;
-            tp[b >> 2] |= (k0 ? t_ : 63u) << (6 * (b & 3));
-            const float *w0 = sW0 + (k0 ? t_ : (uint32_t)d_in) * FH1 + j;
-            const float z0a = w0[0], z0b = w0[16];
-            const int ab = abase0 + s * NC * RS + 4 * b;
-            const float a0 = W[ab];
-            d1[s][0][0] = mfma4(a0, z0a, d1[s][0][0]);
-            d1[s][0][1] = mfma4(a0, z0b, d1[s][0][1]);
-            if (T > 1) {
-              const float a1 = W[ab + 16 * RS];
-              d1[s][1][0] = mfma4(a1, z0a, d1[s][1][0]);
-              d1[s][1][1] = mfma4(a1, z0b, d1[s][1][1]);
-            }
-          } else {
-            tp[b >> 2] |= 63u << (6 * (b & 3));
-          }
-        }
-  #endif
         tyA[s][0] = tp[0];
         tyA[s][1] = tp[1];
       }
@@ -725,7 +665,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
           }
         }
       };
-  #if SG32_NTN_KR
       if constexpr (T0 == 2) {
         if (KB0 > 6) ntn_fwd(std::integral_constant<int, 8>{});
         else ntn_fwd(std::integral_constant<int, 6>{});
@@ -733,10 +672,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
         if (KB0 > 2) ntn_fwd(std::integral_constant<int, 4>{});
         else ntn_fwd(std::integral_constant<int, 2>{});
       }
-  #else
-      ntn_fwd(std::integral_constant<int, 8>{});   // (KR = 8: every row read)
-  #endif
-  #if SG32_V_HOIST >= 1
       // V entries of the lane's rows, read unconditionally (one LDS round trip; rows past
       // the sides' k-blocks are never used): vu = u + V[k][a] (forward and ∂L/∂x1)
       float vu[8], vb[8];
@@ -753,22 +688,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
         if (kb_live(rr, T0, KB0)) mpart = fmaf(xo[0][rr], vu[rr], mpart);
         if (kb_live(rr, T1, KB1)) mpart = fmaf(xo[1][rr], vb[rr], mpart);
       }
-  #else
-      float mpart = 0.f;
-  #pragma unroll
-      for (int rr = 0; rr < 8; ++rr) {
-        if (kb_live(rr, T0, KB0)) {
-          const int a = 4 * rr + g;
-          const int ac = a < D ? a : 0;
-          mpart = fmaf(xo[0][rr], u[rr] + sV[kc * VS + ac], mpart);
-        }
-        if (kb_live(rr, T1, KB1)) {
-          const int b = 4 * rr + g;
-          const int bc = b < D ? b : 0;
-          mpart = fmaf(xo[1][rr], sV[kc * VS + D + bc], mpart);
-        }
-      }
-  #endif
       const float m = xsum32(xsum16(mpart)) + bnk;
       const float rk = (kv & (m > 0.f)) ? m : 0.f;
       const float rsum = row_sum16(rk);
@@ -800,39 +719,20 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
         if (g == 0) nb_[2 * NC + j] = gmk;
       }
       const float gmk4 = gmk * A.ik4;
-  #if SG32_V_HOIST >= 2
-      // the V entries of side 1's rows read unconditionally (one LDS round trip)
-      float vb2[8];
-  #pragma unroll
-      for (int rr = 0; rr < 8; ++rr) {
-        const int b = 4 * rr + g;
-        vb2[rr] = sV[kc * VS + D + (b < D ? b : 0)];
-      }
-  #endif
       float ge[2][8];   // dL/dx · ik4 (before the x > 0 mask) of the lane's rows
   #pragma unroll
       for (int rr = 0; rr < 8; ++rr) {
         ge[0][rr] = ge[1][rr] = 0.f;
         if (kb_live(rr, T0, KB0)) {
-  #if SG32_V_HOIST >= 1
           ge[0][rr] = row_sum16(gmk4 * vu[rr]);
-  #else
-          const int a = 4 * rr + g;
-          const int ac = a < D ? a : 0;
-          ge[0][rr] = row_sum16(gmk4 * (sV[kc * VS + ac] + u[rr]));
-  #endif
         }
       }
   #pragma unroll
       for (int rr = 0; rr < 8; ++rr) {
         if (kb_live(rr, T1, KB1)) {
-  #if SG32_V_HOIST >= 2
-          ge[1][rr] = row_sum16(gmk4 * (vb2[rr] + cs[rr]));
-  #else
           const int b = 4 * rr + g;
           const int bc = b < D ? b : 0;
           ge[1][rr] = row_sum16(gmk4 * (sV[kc * VS + D + bc] + cs[rr]));
-  #endif
         }
       }
 
@@ -869,7 +769,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
             for (int b = 0; b < 8; ++b) {
               if (kb_live(b, T, KB)) {
                 gz1[to] = mfma4(af[to][b], gh2[b >> 2][b & 3], gz1[to]);
-                if (!SG32_GZ1T_LDS) gz1t[to] = mfma4(gh2[b >> 2][b & 3], af[to][b], gz1t[to]);
               }
             }
           }
@@ -882,7 +781,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
             for (int f = 0; f < 2; ++f) gw1[f] = mfma4(d1[s][b >> 2][f][b & 3], gz1[b >> 2][b & 3], gw1[f]);
           }
         }
-  #if SG32_GZ1T_LDS
         // gZ1 rows 16 to + 4g + r, feature j into the tile; read back as row 16 to + j,
         // features 4g..4g+3 (the previous side's reads are done: program order)
   #pragma unroll
@@ -894,7 +792,6 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
   #pragma unroll
         for (int to = 0; to < 2; ++to)
           if (to < T) gz1t[to] = *(const f4 *)(sT + (16 * to + j) * TS1 + 4 * g);
-  #endif
         // gD1 · ik1 = gZ1 (W1 ik1)ᵀ; gP1 = keep·relu' (D1 > 0); gZ0 = Âᵀ gP1
         f4 gp1[2][2];   // [to][f]
   #pragma unroll

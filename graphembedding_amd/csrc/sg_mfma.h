@@ -27,11 +27,7 @@ __device__ __forceinline__ uint32_t pk_bf16(float a, float b) {   // v_cvt_pk_bf
   const bf2v v = {(__bf16)a, (__bf16)b};
   return __builtin_bit_cast(uint32_t, v);
 }
-// (x0, x1) -> packed bf16 pairs of the h, m, l parts (x = h + m + l + e)
-#ifndef SG_SPLIT_TRUNC
-#define SG_SPLIT_TRUNC 1
-#endif
-#if SG_SPLIT_TRUNC
+// (x0, x1) -> packed bf16 pairs of the h, m, l parts (x = h + m + l + e).
 // Truncating parts: h = x with the low 16 mantissa bits cleared (one AND), r = x - h and
 // r - m exact in f32, and the bf16 pairs are the high halves of (x0, x1) and of the
 // residuals, packed by v_perm_b32.  |e| < 2^-21 |x| (RNE parts: 2^-24), at 4 ANDs, 4 subs
@@ -67,14 +63,6 @@ __device__ __forceinline__ void split3(float x0, float x1, uint32_t &h, uint32_t
 #endif
   l = hi16x2(__float_as_uint(s0), __float_as_uint(s1));
 }
-#else
-__device__ __forceinline__ void split3(float x0, float x1, uint32_t &h, uint32_t &m, uint32_t &l) {
-  h = pk_bf16(x0, x1);
-  const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xFFFF0000u);
-  m = pk_bf16(r0, r1);
-  l = pk_bf16(r0 - __uint_as_float(m << 16), r1 - __uint_as_float(m & 0xFFFF0000u));
-}
-#endif
 __device__ __forceinline__ f4 mfbf(uint4 a, uint4 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a),
                                                   __builtin_bit_cast(bf8, b), c, 0, 0, 0);

@@ -30,6 +30,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <list>
 #include <mutex>
 #include <type_traits>
 #include <vector>
@@ -50,10 +51,7 @@ constexpr int TB = 128;             // GEMM tile edge
 constexpr int MKS = 20;             // MK LDS tile row stride (16 + 4): conflict-free b128 reads
 constexpr int KMS = TB + 4;         // KM LDS tile row stride
 constexpr int HSLAB = 1 + 2 * WKP;  // head slab row: loss | gU[16] | gb[16]
-#ifndef SG_WEB_WSPLIT
-#define SG_WEB_WSPLIT 16
-#endif
-constexpr int WSPLIT = SG_WEB_WSPLIT;   // split-K over pairs of the weight-gradient GEMMs
+constexpr int WSPLIT = 16;   // split-K over pairs of the weight-gradient GEMMs
 constexpr int kUnitChunk = 4096;    // instances per block of the size-class sort (web_icls_*)
 // XCD partitions of the instance units: instances of graph g go to partition g % kXcdParts,
 // and unit slot u runs on the workgroups with blockIdx.x = u (mod kXcdParts), which the
@@ -158,26 +156,13 @@ struct WebWs {
 };
 
 int gcn_blocks_for() { return sg_num_cus(); }
-#ifndef SG_WEB_HEAD_BPC
-#define SG_WEB_HEAD_BPC 3
-#endif
-int head_blocks_for() { return SG_WEB_HEAD_BPC * sg_num_cus(); }
+int head_blocks_for() { return 3 * sg_num_cus(); }
 
-#ifndef SG_WEB_T_BF3
-#define SG_WEB_T_BF3 1
-#endif
 
 // The backward instance kernel reads the dropout keep bits the forward wrote (GcnArgs::masks)
 // instead of re-hashing 13 elements per lane and tile; 0: it re-hashes (A/B)
-#ifndef SG_WEB_MASKS
-#define SG_WEB_MASKS 1
-#endif
 // ... and the forward's D2 = dropout(H2) rows (GcnArgs::d2) instead of recomputing Z1 = D1'·W1
 // and the H2 pass, which also drops two of the unit's barriers; 0: it recomputes (A/B)
-#ifndef SG_WEB_D2
-#define SG_WEB_D2 1
-#endif
-static_assert(!SG_WEB_D2 || SG_WEB_MASKS, "the D2 rows need the keep bits");
 
 WebWs web_ws(const WebPlan &W, int64_t chunk) {
   WebWs w;
@@ -201,7 +186,7 @@ WebWs web_ws(const WebPlan &W, int64_t chunk) {
   w.X = take(2 * w.Cp * Dp);        // X1 | X2
   w.GX = take(2 * w.Cp * Dp);       // gX1 | gX2
   // T: the a-tile shares MP[p][k][4] of web_t_kernel_b3<true>, or all of T (f32 path)
-  w.T = take(SG_WEB_T_BF3 ? w.Cp * WKP * 4 : w.Cp * K * Dp);
+  w.T = take(w.Cp * WKP * 4);
   w.GM = take(w.Cp * WKP);
   w.EXT = take(2 * w.Cp);           // int2 per pair
   w.EXT16 = take(2 * (w.Cp / 16));
@@ -211,7 +196,7 @@ WebWs web_ws(const WebPlan &W, int64_t chunk) {
   w.ICNT = take(kIKeys * ((2 * w.Cp + kUnitChunk - 1) / kUnitChunk));
   w.ICLS = take(kIKeys + 8);
   w.MASK = take(4 * w.Cp * Dp);     // 2 Cp x Dp x 4 uint16
-  w.D2 = SG_WEB_D2 ? take(32 * w.Cp * Dp) : 0;   // 2 Cp x Dp x 16
+  w.D2 = take(32 * w.Cp * Dp);   // 2 Cp x Dp x 16
   w.SLOT = o;
   w.total1 = w.S0 + w.SLOT;
   w.total = w.S0 + 2 * w.SLOT;
@@ -421,22 +406,13 @@ __global__ void __launch_bounds__(256) web_wprep_h(const float *__restrict__ Wg,
 // t % waves (N <= 512: 32 tiles).  The sparse loops read the instance's CSR rows
 // through the caches; LCSR (opt-in) stages them in LDS first.
 // ---------------------------------------------------------------------------
-// waves per instance workgroup: SG_WEB_FWD_WAVES forward, SG_WEB_BWD_WAVES backward.
+// waves per instance workgroup: 8 forward, 16 backward.
 // The backward wants more than the 128 VGPRs of a 16-wave block and spills ~32 of them
 // there, but twice the waves per instance hide the latency-bound sparse phases better:
 // 16 waves measured 411 -> 379 ms per C5 step against 8 (246 VGPRs, no spills).
-#ifndef SG_WEB_BWD_WAVES
-#define SG_WEB_BWD_WAVES 16
-#endif
 // forward instance kernel: 8 waves (4 tiles each) measured 3.596 vs 3.571 M pairs/s
 // against 16 on C5 (one stream), 3.610 with the chunk pipeline (profiles/r03_c5fw8/)
-#ifndef SG_WEB_FWD_WAVES
-#define SG_WEB_FWD_WAVES 8
-#endif
-#ifndef SG_WEB_FWD_BPC_DEF
-#define SG_WEB_FWD_BPC_DEF 2
-#endif
-__host__ __device__ constexpr int gcn_gw(bool bwd) { return bwd ? SG_WEB_BWD_WAVES : SG_WEB_FWD_WAVES; }
+__host__ __device__ constexpr int gcn_gw(bool bwd) { return bwd ? 16 : 8; }
 
 struct GcnArgs {
   const int32_t *node_off, *types, *row_ptr, *col;
@@ -487,18 +463,12 @@ constexpr int SCS = 20, SCR = 16 * SCS;
 // gS0 = Â·gP0 with one CSR row per lane (node 16t + i, features 16c + 4g + s) and the tile
 // transposed through the wave's scratch for the one-hot gW0 MFMA; 0: four rows per lane
 // (nodes 16t + 4g + s, features i, 16 + i), the MFMA layout directly
-#ifndef SG_WEB_GS0_ROW
-#define SG_WEB_GS0_ROW 1
-#endif
 // Backward MFMAs on split-bf16 (round 4): gD1 = gS1·W1ᵀ as three v_mfma_f32_16x16x32_bf16
 // per feature half against W1's bf16 parts built once per block (the six leading products
 // of (h + m + l)(H + M + L), ≈ f32 accuracy; sg_fast's gD1), and the one-hot gW0 = Xᵀ·gS0 as
 // three v_mfma_f32_16x16x16_bf16 per (type tile, feature half) on the h, m and l parts of
 // gS0 (one-hot is exact in bf16) — 16-cycle / 8-cycle bf16 MFMAs that co-issue with VALU in
 // place of 32-cycle f32 ones that do not.  0: the f32 MFMAs (A/B)
-#ifndef SG_WEB_BF16_BWD
-#define SG_WEB_BF16_BWD 1
-#endif
 
 struct GcnLds {
   int w0, b0, w1, w1t, b1, wd, w1b, tables, et, gx, z1, d1, scr, rp, col, val, total;
@@ -514,8 +484,8 @@ __host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, int max_nnz, bool b
   L.b1 = o; o += WH2;
   L.wd = o; o += WH2;
   o = (o + 3) & ~3;
-  // backward: [cb][term][lane] uint4 bf16 B operands of gD1 (SG_WEB_BF16_BWD)
-  L.w1b = o; if (bwd && SG_WEB_BF16_BWD) o += 2 * 3 * 64 * 4;
+  // backward: [cb][term][lane] uint4 bf16 B operands of gD1
+  L.w1b = o; if (bwd) o += 2 * 3 * 64 * 4;
   L.tables = o;
   L.et = o; o += n16;
   L.gx = o; if (bwd) o += n16;
@@ -530,46 +500,15 @@ __host__ __device__ inline GcnLds gcn_lds(int d_in, int n16, int max_nnz, bool b
 }
 
 
-// Σ_e val[e] · f(col[e]) over one CSR row.  SG_WEB_ROWP = 0 (default): four neighbours'
-// loads in flight at a time, then the tail one entry at a time; SG_WEB_ROWP = w > 0: w
-// entries per step with no branch inside the step (indices past the row clamped to its last
-// entry, their value read as 0: fmaf(0, x, acc) = acc), so a row of up to w entries is one
-// global round trip.  Measured on C5 (profiles/r03_c5ab/): w = 4 2.97, w = 8 2.65 against
-// 3.88 M pairs/s, and eight entries with a branch around each call 3.20: the padded entries'
-// LDS gathers cost more than the round trips they save.
-#ifndef SG_WEB_ROWP
-#define SG_WEB_ROWP 0
-#endif
-// the CSR row extents of a lane's rows loaded once per unit (1) or before each row's
-// gather (0)
-#ifndef SG_WEB_ROW_EXT
-#define SG_WEB_ROW_EXT 1
-#endif
-// csr_row's tail of fewer than four entries: a pair, then a single (1), or one at a time (0)
-#ifndef SG_WEB_TAIL2
-#define SG_WEB_TAIL2 1
-#endif
+// Σ_e val[e] · f(col[e]) over one CSR row: four neighbours' loads in flight at a time,
+// then a tail of a pair and a single.  (Measured and dropped on C5, profiles/r03_c5ab/: w
+// entries per branch-free step with indices past the row clamped, w = 4 2.97 and w = 8 2.65
+// against 3.88 M pairs/s; the padded entries' LDS gathers cost more than the round trips
+// they save.)  The CSR row extents of a lane's rows are loaded once per unit.
 template <typename CT, typename F>
 __device__ __forceinline__ void csr_row(const CT *__restrict__ col, const float *__restrict__ val,
                                         int e0, int e1, F f) {
   int e = e0;
-#if SG_WEB_ROWP > 0
-  constexpr int RW = SG_WEB_ROWP;
-  for (; e < e1; e += RW) {
-    int c[RW];
-    float v[RW];
-#pragma unroll
-    for (int k = 0; k < RW; ++k) {
-      const bool in = e + k < e1;
-      const int ek = in ? e + k : e1 - 1;
-      c[k] = col[ek];
-      const float x = val[ek];
-      v[k] = in ? x : 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < RW; ++k) f(c[k], v[k]);
-  }
-#else
   for (; e + 4 <= e1; e += 4) {
     const int c0 = col[e], c1 = col[e + 1], c2 = col[e + 2], c3 = col[e + 3];
     const float v0 = val[e], v1 = val[e + 1], v2 = val[e + 2], v3 = val[e + 3];
@@ -578,7 +517,6 @@ __device__ __forceinline__ void csr_row(const CT *__restrict__ col, const float 
     f(c2, v2);
     f(c3, v3);
   }
-#if SG_WEB_TAIL2
   // a tail of 2-3 entries as a pair then a single (two dependent round trips, not three)
   if (e + 2 <= e1) {
     const int c0 = col[e], c1 = col[e + 1];
@@ -588,10 +526,6 @@ __device__ __forceinline__ void csr_row(const CT *__restrict__ col, const float 
     e += 2;
   }
   if (e < e1) f(col[e], val[e]);
-#else
-  for (; e < e1; ++e) f(col[e], val[e]);
-#endif
-#endif
 }
 
 // instance (.x, -1: none) of wave w in unit slot u of the partitioned size-class order
@@ -611,15 +545,10 @@ __device__ __forceinline__ int2 web_unit_q(int u, const int32_t *isorted, const 
   return make_int2((u < n_units && s0 + kk < end) ? isorted[s0 + kk] : -1, gsz);
 }
 
-// the forward's keep draws (the backward reads them back, SG_WEB_MASKS); SG_WEB_ABL_FHASH
-// (timing ablation only, results invalid) replaces the hash by one compare
+// the forward's keep draws (the backward reads them back)
 __device__ __forceinline__ bool web_fkeep(uint32_t pk, uint32_t layer, uint32_t side, uint32_t e,
                                           uint32_t thr) {
-#ifdef SG_WEB_ABL_FHASH
-  return ((pk ^ e ^ layer ^ side) & 0xFFFFu) < thr;
-#else
   return sg_keep(pk, layer, side, e, thr);
-#endif
 }
 
 template <bool BWD, int NTB, bool LCSR>
@@ -647,7 +576,6 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
     sW1[x] = v;
     sW1T[(x % WH2) * WH1 + x / WH2] = v;
   }
-#if SG_WEB_BF16_BWD
   // gD1's B operands: lane (i, g) of feature half cb holds the parts of
   // W1[16cb + i][4g..4g+3]·ik1 as (H | H), (M | H), (L | M) (k-slots 8g..8g+7)
   uint4 *sW1B = (uint4 *)(sm + L.w1b);
@@ -661,7 +589,6 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
       sW1B[x] = term == 0 ? uint4{h01, h23, h01, h23}
                           : (term == 1 ? uint4{m01, m23, h01, h23} : uint4{l01, l23, m01, m23});
     }
-#endif
   if (tid < WH1) sb0[tid] = prm[A.ob0 + tid];
   if (tid < WH2) {
     sb1[tid] = prm[A.ob1 + tid];
@@ -758,8 +685,8 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
     // dropout keep bits of this lane's tiles: the backward loads the forward's (their
     // latency overlaps the staging below), the forward builds them
     uint32_t mw[GCN_TPW];
-    constexpr bool use_mw = BWD && SG_WEB_MASKS;   // sg_web_run passes masks then
-    constexpr bool use_d2 = BWD && SG_WEB_D2;      // ... and the D2 rows
+    constexpr bool use_mw = BWD;   // sg_web_run passes masks then
+    constexpr bool use_d2 = BWD;   // ... and the D2 rows
     f4 d2v[GCN_TPW];
 #pragma unroll
     for (int u = 0; u < GCN_TPW; ++u) {
@@ -803,15 +730,15 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
 #pragma unroll
     for (int u = 0; u < GCN_TPW; ++u) {
       const int n = 16 * (lw + u * WPI) + i;
-      const bool in_ = SG_WEB_ROW_EXT && n < N;
+      const bool in_ = n < N;
       re0[u] = in_ ? rp[n] : 0;
       re1[u] = in_ ? rp[n + 1] : 0;
     }
     auto row0 = [&](int u, int n) __attribute__((always_inline)) -> int {
-      return SG_WEB_ROW_EXT ? re0[u] : rp[n];
+      return re0[u];
     };
     auto row1 = [&](int u, int n) __attribute__((always_inline)) -> int {
-      return SG_WEB_ROW_EXT ? re1[u] : rp[n + 1];
+      return re1[u];
     };
 
     // ---- forward: H1 (lane (i, g): node 16t+i, features 16c + 4g + s), D1', Z1 ----
@@ -827,9 +754,6 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
         h[4 * c] = b.x; h[4 * c + 1] = b.y; h[4 * c + 2] = b.z; h[4 * c + 3] = b.w;
       }
       if (n < N) {
-#ifdef SG_WEB_ABL_FH1   // timing ablation only (results invalid): the forward skips the H1 gather
-        if (BWD)
-#endif
         csr_row(cl, vl, row0(u, n), row1(u, n), [&](int mm, float v) {
           const float *wr = sW0 + sEtk[mm] * W0S + 4 * g;
           const float4 wa = *(const float4 *)wr, wb = *(const float4 *)(wr + 16);
@@ -889,9 +813,6 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
         h2[0] = b.x; h2[1] = b.y; h2[2] = b.z; h2[3] = b.w;
 #ifdef SG_WEB_ABL_NOH2   // timing ablation only (results invalid): the backward skips the H2 pass
         if (!BWD)
-#endif
-#ifdef SG_WEB_ABL_FH2   // timing ablation only (results invalid): the forward skips the H2 gather
-        if (BWD)
 #endif
         csr_row(cl, vl, row0(u, n), row1(u, n), [&](int mm, float v) {
           const float4 zz = *(const float4 *)(sZ1k + mm * ZS + 4 * g);
@@ -970,7 +891,6 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
         });
       // gD1·ik1 (rows n = 16t + 4g + r, column f = 16cb + i)
       f4 gd[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
-#if SG_WEB_BF16_BWD
       {   // A k-slots 8g..8g+7 = (h | m) or (h | l) of gS1[n][4g..4g+3]: hH + mH + hM + lH + hL + mM
         uint32_t h01, m01, l01, h23, m23, l23;
         sgk::split3(q4[0], q4[1], h01, m01, l01);
@@ -984,12 +904,6 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
           gd[cb] = sgk::mfbf(ahm, wb[128], gd[cb]);
         }
       }
-#else
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) gd[cb] = mfma4(q4[s], sW1T[(4 * g + s) * WH1 + 16 * cb + i], gd[cb]);
-#endif
       // the tile's gS1 through the wave's scratch, read back as the B operand of gW1
       *(float4 *)(scr + i * SCS + 4 * g) = make_float4(q4[0], q4[1], q4[2], q4[3]);
       sg_wsync();
@@ -1019,7 +933,6 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
     for (int u = 0; u < GCN_TPW; ++u) {
       const int t = lw + u * WPI;
       if (t >= ntile) break;
-#if SG_WEB_GS0_ROW
       // one CSR row per lane: node n = 16t + i, features 16c + 4g + s (two b128 reads of
       // the gP0 row per entry); dropped and absent nodes (et = d_in) contribute zero
       float hq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1038,7 +951,6 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
       int et[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) et[s] = sEtk[16 * t + 4 * g + s];
-#if SG_WEB_BF16_BWD
       // one-hot Xᵀ as a bf16 A operand: row i ↔ type 16tb + i, k-slot 4g + s ↔ node
       // 16t + 4g + s (v_mfma_f32_16x16x16_bf16: 4 k-slots per lane)
       uint2 oh[NTB];
@@ -1049,7 +961,6 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
         for (int s = 0; s < 4; ++s) o[s] = et[s] == 16 * tb + i ? 0x3F80u : 0u;   // bf16 1.0
         oh[tb] = uint2{o[0] | (o[1] << 16), o[2] | (o[3] << 16)};
       }
-#endif
       // per feature half c: the tile through the scratch, read back as the B operand
       // (k-slot g ↔ node 16t + 4g + s, column i ↔ feature 16c + i)
 #pragma unroll
@@ -1062,7 +973,6 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) bq[s] = scr[(4 * g + s) * SCS + i];
         sg_wsync();
-#if SG_WEB_BF16_BWD
         uint32_t h01, m01, l01, h23, m23, l23;
         sgk::split3(bq[0], bq[1], h01, m01, l01);
         sgk::split3(bq[2], bq[3], h23, m23, l23);
@@ -1072,41 +982,7 @@ __global__ void __launch_bounds__(64 * gcn_gw(BWD)) web_gcn_kernel(GcnArgs A) {
           aW0[tb][c] = sgk::mfbf16(oh[tb], uint2{m01, m23}, aW0[tb][c]);
           aW0[tb][c] = sgk::mfbf16(oh[tb], uint2{h01, h23}, aW0[tb][c]);
         }
-#else
-#pragma unroll
-        for (int tb = 0; tb < NTB; ++tb)
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            const float a = et[s] == 16 * tb + i ? 1.f : 0.f;
-            aW0[tb][c] = mfma4(a, bq[s], aW0[tb][c]);
-          }
-#endif
       }
-#else
-      float bq[4][2];
-      int et[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int n = 16 * t + 4 * g + s;
-        float q0 = 0.f, q1 = 0.f;
-        et[s] = sEtk[n];
-        if (n < N && et[s] < d_in)
-          csr_row(cl, vl, rp[n], rp[n + 1], [&](int mm, float v) {
-            q0 = fmaf(v, sD1k[mm * DS + i], q0);
-            q1 = fmaf(v, sD1k[mm * DS + 16 + i], q1);
-          });
-        bq[s][0] = q0 * A.ik0;   // scale0 = keep0 · ik0 (dropped nodes: et = d_in, q = 0)
-        bq[s][1] = q1 * A.ik0;
-      }
-#pragma unroll
-      for (int tb = 0; tb < NTB; ++tb)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const float a = et[s] == 16 * tb + i ? 1.f : 0.f;
-          aW0[tb][0] = mfma4(a, bq[s][0], aW0[tb][0]);
-          aW0[tb][1] = mfma4(a, bq[s][1], aW0[tb][1]);
-        }
-#endif
     }
     in = inn;
     q = qn;
@@ -1216,58 +1092,7 @@ __device__ __forceinline__ void mma_km_km(Tile &T, const float *sA, const float 
   }
 }
 
-// ---- T[p][k][a] = Σ_b W[a][b][k] x2[p][b]  (grid: p-blocks × a-tiles × k) ----
-__global__ void __launch_bounds__(256) web_t_kernel(const float *__restrict__ X2,
-                                                    const float *__restrict__ Wg,
-                                                    const int2 *__restrict__ ext128, int64_t n,
-                                                    int Dp, int K, float *__restrict__ Tout) {
-  __shared__ __attribute__((aligned(16))) float sA[TB * MKS], sB[TB * MKS];
-  const int64_t p0 = (int64_t)blockIdx.x * TB;
-  const int a0 = blockIdx.y * TB, k = blockIdx.z;
-  const int2 e = ext128[blockIdx.x];
-  if (a0 >= e.x) return;
-  const int nb = (e.y + 15) & ~15;
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, i = l & 15, g = l >> 4;
-  const int wm = w >> 1, wn = w & 1;
-  const float *pa = X2 + p0 * Dp;
-  const float *pb = Wg + ((size_t)k * Dp + a0) * Dp;
-  float4 ra[2], rb[2];
-  auto load = [&](int b0) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int q = tid + 256 * u, r = q >> 2, sg = (q & 3) * 4;
-      ra[u] = *(const float4 *)(pa + (size_t)r * Dp + b0 + sg);
-      rb[u] = *(const float4 *)(pb + (size_t)r * Dp + b0 + sg);
-    }
-  };
-  Tile T;
-  T.zero();
-  if (nb > 0) load(0);
-  for (int b0 = 0; b0 < nb; b0 += 16) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int q = tid + 256 * u, r = q >> 2, sg = (q & 3) * 4;
-      *(float4 *)(sA + r * MKS + sg) = ra[u];
-      *(float4 *)(sB + r * MKS + sg) = rb[u];
-    }
-    __syncthreads();
-    if (b0 + 16 < nb) load(b0 + 16);
-    mma_mk_mk(T, sA, sB, wm, wn, i, g);
-    __syncthreads();
-  }
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t p = p0 + wm * 64 + mi * 16 + 4 * g + r;
-      if (p >= n) continue;
-      float *dst = Tout + ((size_t)p * K + k) * Dp + a0 + wn * 64 + i;
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) dst[ni * 16] = T.c[mi][ni][r];
-    }
-}
-
-// ---- the same T on bf16 MFMAs (SG_WEB_T_BF3, default): both operands are split on the
+// ---- T on bf16 MFMAs: both operands are split on the
 // fly into three bf16 parts (x = h + m + l, sgk::split3: |x - h - m - l| < 2^-21 |x|)
 // and T accumulates hh + hm + mh + hl + lh + mm in f32 on v_mfma_f32_16x16x32_bf16:
 // 6 MFMAs of 16 cycles per 32-deep product instead of 8 f32 MFMAs of 32 cycles.
@@ -1276,42 +1101,22 @@ __global__ void __launch_bounds__(256) web_t_kernel(const float *__restrict__ X2
 // the next chunk's f32 operands prefetched into registers during the MFMAs.
 constexpr int B3K = 32, B3S = 40;   // contraction chunk, LDS row stride (bf16)
 
-// Block order of the pair-block GEMMs.  SG_WEB_GXCD = 1: a 1-D grid where the NT column
+// Block order of the pair-block GEMMs.  (Measured and dropped: a 1-D grid where the NT column
 // tiles of pair block pb (and, for T, each k, slowest) run on blocks L ≡ pb (mod 8), which
 // the dispatcher deals to one XCD, so that the pair block's x rows would come into that
 // XCD's L2 once for all its tiles.  Measured 3.82-3.84 against 4.21-4.22 M pairs/s on C5
-// (profiles/r03_c5ab/gemm_*), so the default is the (pair block, tile, k) grid.
-#ifndef SG_WEB_GXCD
-#define SG_WEB_GXCD 0
-#endif
+// (profiles/r03_c5ab/gemm_*).)  The grid is (pair block, tile, k).
 __device__ __forceinline__ void web_pb_tile(int NT, int G8, int &pb, int &tile, int &kk) {
-#if SG_WEB_GXCD
-  const int L = (int)blockIdx.x;
-  int rest = L >> 3;
-  tile = rest % NT;
-  rest /= NT;
-  pb = (rest % G8) * 8 + (L & 7);
-  kk = rest / G8;
-#else
   pb = (int)blockIdx.x;
   tile = (int)blockIdx.y;
   kk = (int)blockIdx.z;
-#endif
 }
 static dim3 web_pb_grid(int64_t nblk, int NT, int K) {
-#if SG_WEB_GXCD
-  const int64_t G8 = (nblk + 7) / 8;
-  return dim3((unsigned)(G8 * NT * 8 * K));
-#else
   return dim3((unsigned)nblk, (unsigned)NT, (unsigned)K);
-#endif
 }
 // gX1 / gX2 GEMMs: the contraction runs over (32-deep chunk, k) with k inner, so a chunk's
-// x rows are loaded once and rescaled by gm[p][k] for each k (SG_WEB_GX_KIN=0: k outer, the
-// chunk reloaded per k; 4.19-4.20 against 4.21-4.22 M pairs/s on C5)
-#ifndef SG_WEB_GX_KIN
-#define SG_WEB_GX_KIN 1
-#endif
+// x rows are loaded once and rescaled by gm[p][k] for each k (k outer, the chunk reloaded
+// per k, measured 4.19-4.20 against 4.21-4.22 M pairs/s on C5)
 constexpr int B3PART = TB * B3S;    // bf16 per part plane
 
 __device__ __forceinline__ void b3_split_store(uint16_t *plane, int r, int c, float4 x) {
@@ -1424,7 +1229,7 @@ __global__ void __launch_bounds__(256) web_t_kernel_b3(const float *__restrict__
     }
 }
 
-// ---- T with TKG feature maps k per block (round 4, SG_WEB_TKG, default): web_t_kernel_b3
+// ---- T with TKG feature maps k per block (round 4; SG_WEB_TKG=0 at run time: web_t_kernel_b3): web_t_kernel_b3
 // re-fetched a pair block's x2 rows for each of its K x (a-tiles) tiles (18.45 GB per
 // 524,288-pair chunk against ≈0.5 GB of x rows, rocprof FETCH_SIZE).  Here one 8-wave block
 // stages the x2 chunk once for TKG = 4 feature maps k (the B operands of the four W[k]
@@ -1432,9 +1237,6 @@ __global__ void __launch_bounds__(256) web_t_kernel_b3(const float *__restrict__
 // a-tile instead of K times.  Wave w: k = 4 kg + 2 (w >> 2) + {0, 1}, 64x64 sub-tile
 // ((w >> 1) & 1, w & 1).  Per (k, tile) the MFMA order is web_t_kernel_b3's, so MP is bitwise
 // the same.
-#ifndef SG_WEB_TKG
-#define SG_WEB_TKG 1
-#endif
 constexpr int TKG = 4;
 __global__ void __launch_bounds__(512) web_t_kernel_kg(const float *__restrict__ X2,
                                                        const float *__restrict__ Wg,
@@ -1551,62 +1353,6 @@ __global__ void __launch_bounds__(512) web_t_kernel_kg(const float *__restrict__
   }
 }
 
-// ---- gX2[p][b] += Σ_{k,a} gm[p][k] x1[p][a] W[a][b][k]  (grid: p-blocks × b-tiles) ----
-__global__ void __launch_bounds__(256) web_gx2_kernel(const float *__restrict__ X1,
-                                                      const float *__restrict__ GM,
-                                                      const float *__restrict__ Wh,
-                                                      const int2 *__restrict__ ext128, int64_t n,
-                                                      int Dp, int K, float *__restrict__ GX2) {
-  __shared__ __attribute__((aligned(16))) float sA[TB * MKS], sB[TB * MKS];
-  const int64_t p0 = (int64_t)blockIdx.x * TB;
-  const int b0 = blockIdx.y * TB;
-  const int2 e = ext128[blockIdx.x];
-  if (b0 >= e.y) return;
-  const int na = (e.x + 15) & ~15;
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, i = l & 15, g = l >> 4;
-  const int wm = w >> 1, wn = w & 1;
-  float4 ra[2], rb[2];
-  float gmr[2];
-  auto load = [&](int k, int a0) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int q = tid + 256 * u, r = q >> 2, sg = (q & 3) * 4;
-      const int64_t p = p0 + r;
-      gmr[u] = p < n ? GM[p * WKP + k] : 0.f;
-      ra[u] = *(const float4 *)(X1 + p * Dp + a0 + sg);
-      rb[u] = *(const float4 *)(Wh + ((size_t)k * Dp + b0 + r) * Dp + a0 + sg);
-    }
-  };
-  Tile T;
-  T.zero();
-  const int steps = na / 16, total = K * steps;
-  if (total > 0) load(0, 0);
-  for (int st = 0; st < total; ++st) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int q = tid + 256 * u, r = q >> 2, sg = (q & 3) * 4;
-      const float gm = gmr[u];
-      *(float4 *)(sA + r * MKS + sg) =
-          make_float4(gm * ra[u].x, gm * ra[u].y, gm * ra[u].z, gm * ra[u].w);
-      *(float4 *)(sB + r * MKS + sg) = rb[u];
-    }
-    __syncthreads();
-    if (st + 1 < total) load((st + 1) / steps, ((st + 1) % steps) * 16);
-    mma_mk_mk(T, sA, sB, wm, wn, i, g);
-    __syncthreads();
-  }
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t p = p0 + wm * 64 + mi * 16 + 4 * g + r;
-      if (p >= n) continue;
-      float *dst = GX2 + p * Dp + b0 + wn * 64 + i;
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) dst[ni * 16] += T.c[mi][ni][r];
-    }
-}
-
 // ---- gX2 on bf16 MFMAs (as web_t_kernel_b3): A = gm[p][k] x1[p][a] scaled while
 // staging, B = Wh[k][b][a]; 32-deep chunks of a for each k ----
 __global__ void __launch_bounds__(256) web_gx2_kernel_b3(const float *__restrict__ X1,
@@ -1656,8 +1402,7 @@ __global__ void __launch_bounds__(256) web_gx2_kernel_b3(const float *__restrict
     __syncthreads();
     if (st + 1 < total) {
       const int s1 = st + 1;
-      if (SG_WEB_GX_KIN) load(s1 % K, (s1 / K) * B3K, s1 % K == 0);
-      else load(s1 / steps, (s1 % steps) * B3K, true);
+      load(s1 % K, (s1 / K) * B3K, s1 % K == 0);
     }
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
@@ -1690,89 +1435,6 @@ __global__ void __launch_bounds__(256) web_gx2_kernel_b3(const float *__restrict
       float *dst = GX2 + p * Dp + b0 + wn * 64 + i;
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) dst[ni * 16] += acc[mi][ni][r];
-    }
-}
-
-// ---- gWs[s][k][a][b] += Σ_{p in split s} gm[p][k] x1[p][a] x2[p][b]
-//      (grid: a-tile·b-tile × k × split) ----
-__global__ void __launch_bounds__(256) web_wgrad_kernel(const float *__restrict__ X1,
-                                                        const float *__restrict__ X2,
-                                                        const float *__restrict__ GM,
-                                                        const int2 *__restrict__ ext16, int64_t n,
-                                                        int Dp, int K, float *__restrict__ GWS) {
-  __shared__ __attribute__((aligned(16))) float sA[16 * KMS], sB[16 * KMS];
-  const int nbt = Dp / TB;
-  const int a0 = (blockIdx.x / nbt) * TB, b0 = (blockIdx.x % nbt) * TB;
-  const int k = blockIdx.y, s = blockIdx.z;
-  const int64_t nc = (n + 15) / 16;   // 16-pair chunks of the batch
-  const int64_t c0 = nc * s / WSPLIT, c1 = nc * (s + 1) / WSPLIT;
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, i = l & 15, g = l >> 4;
-  const int wm = w >> 1, wn = w & 1;
-  // Active 16-pair chunks (some pair reaches this tile) are compacted in order into
-  // an LDS list, a window of 1024 raw chunks at a time, so the main loop can
-  // prefetch the next active chunk into registers while the current one computes.
-  __shared__ int act[1024];
-  __shared__ int wcnt[4];
-  auto stage = [&](float4 (&ra)[2], float4 (&rb)[2], int64_t c) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int q = tid + 256 * u, r = q >> 5, cc = (q & 31) * 4;
-      const int64_t p = c * 16 + r;
-      ra[u] = rb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (p < n) {
-        const float gm = GM[p * WKP + k];
-        const float4 x = *(const float4 *)(X1 + p * Dp + a0 + cc);
-        ra[u] = make_float4(gm * x.x, gm * x.y, gm * x.z, gm * x.w);
-        rb[u] = *(const float4 *)(X2 + p * Dp + b0 + cc);
-      }
-    }
-  };
-  Tile T;
-  T.zero();
-  for (int64_t wbase = c0; wbase < c1; wbase += 1024) {
-    int na = 0;
-    for (int r0 = 0; r0 < 1024 && wbase + r0 < c1; r0 += 256) {
-      const int64_t c = wbase + r0 + tid;
-      bool on = false;
-      if (c < c1) {
-        const int2 e = ext16[c];
-        on = e.x > a0 && e.y > b0;
-      }
-      const uint64_t bal = __ballot(on);
-      const int before = __popcll(bal & ((1ull << l) - 1ull));
-      if (l == 0) wcnt[w] = __popcll(bal);
-      __syncthreads();
-      int off = na;
-      for (int u = 0; u < w; ++u) off += wcnt[u];
-      if (on) act[off + before] = (int)(r0 + tid);
-      na += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-      __syncthreads();
-    }
-    if (na == 0) continue;
-    float4 ra[2], rb[2];
-    stage(ra, rb, wbase + act[0]);
-    for (int x = 0; x < na; ++x) {
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int q = tid + 256 * u, r = q >> 5, cc = (q & 31) * 4;
-        *(float4 *)(sA + r * KMS + cc) = ra[u];
-        *(float4 *)(sB + r * KMS + cc) = rb[u];
-      }
-      __syncthreads();
-      if (x + 1 < na) stage(ra, rb, wbase + act[x + 1]);
-      mma_km_km(T, sA, sB, wm, wn, i, g);
-      __syncthreads();
-    }
-  }
-  float *base = GWS + (((size_t)s * K + k) * Dp) * Dp;
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int a = a0 + wm * 64 + mi * 16 + 4 * g + r;
-      float *dst = base + (size_t)a * Dp + b0 + wn * 64 + i;
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) dst[ni * 16] += T.c[mi][ni][r];
     }
 }
 
@@ -1826,8 +1488,7 @@ __global__ void __launch_bounds__(256) web_gx1_kernel_b3(const float *__restrict
     __syncthreads();
     if (st + 1 < total) {
       const int s1 = st + 1;
-      if (SG_WEB_GX_KIN) load(s1 % K, (s1 / K) * B3K, s1 % K == 0);
-      else load(s1 / steps, (s1 % steps) * B3K, true);
+      load(s1 % K, (s1 / K) * B3K, s1 % K == 0);
     }
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
@@ -2017,41 +1678,6 @@ __global__ void __launch_bounds__(256) web_wgrad_kernel_b3(const float *__restri
   }
 }
 
-// ---- gVs[s][k][c] += Σ_{p in split s} gm[p][k] x12[p][c]  (c < Dp: x1, else x2) ----
-__global__ void __launch_bounds__(256) web_gv_kernel(const float *__restrict__ X,
-                                                     const float *__restrict__ GM, int64_t n,
-                                                     int64_t Cp, int Dp, int K,
-                                                     float *__restrict__ GVS) {
-  __shared__ float red[4][WKP][64];
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-  const int c = blockIdx.x * 64 + l, s = blockIdx.y;
-  const int64_t q0 = n * s / WSPLIT, q1 = n * (s + 1) / WSPLIT;
-  const float *src = c < Dp ? X + c : X + Cp * Dp + (c - Dp);
-  float acc[WKP];
-#pragma unroll
-  for (int k = 0; k < WKP; ++k) acc[k] = 0.f;
-  for (int64_t p = q0 + w; p < q1; p += 4) {
-    const float x = src[p * Dp];
-    const float4 *gm4 = (const float4 *)(GM + p * WKP);
-#pragma unroll
-    for (int k4 = 0; k4 < WKP / 4; ++k4) {
-      const float4 gm = gm4[k4];
-      acc[4 * k4] = fmaf(gm.x, x, acc[4 * k4]);
-      acc[4 * k4 + 1] = fmaf(gm.y, x, acc[4 * k4 + 1]);
-      acc[4 * k4 + 2] = fmaf(gm.z, x, acc[4 * k4 + 2]);
-      acc[4 * k4 + 3] = fmaf(gm.w, x, acc[4 * k4 + 3]);
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < WKP; ++k) red[w][k][l] = acc[k];
-  __syncthreads();
-  for (int x = tid; x < K * 64; x += 256) {
-    const int k = x >> 6, cl = x & 63;
-    const float v = (red[0][k][cl] + red[1][k][cl]) + (red[2][k][cl] + red[3][k][cl]);
-    GVS[((size_t)s * WKP + k) * 2 * Dp + blockIdx.x * 64 + cl] += v;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Per-pair NTN head: m_k, s, ŷ, loss, gm; gx1 = Σ_k gm_k (T_k + V_k),
 // gx2 := Σ_k gm_k V_k[D + ·] (web_gx2 adds the W term).  One wave per pair.
@@ -2067,9 +1693,6 @@ struct HeadArgs {
   float yeta, inv_batch;
 };
 
-#ifndef SG_WEB_HEAD_TRIM
-#define SG_WEB_HEAD_TRIM 1
-#endif
 // MT: T holds web_t_kernel_b3<true>'s a-tile shares MP[p][k][tile] of Σ_a x1[a] T[k][a]
 // instead of T, and gx1 gets only its V term here (web_gx1_kernel_b3 adds the T term)
 template <bool BWD, bool MT>
@@ -2100,8 +1723,8 @@ __global__ void __launch_bounds__(256) web_head_kernel(HeadArgs A) {
     const int e1 = ex.x;
     // x1 / x2 are zero past the extents (padding 0) and gx past them is never read (the
     // instance kernels take ∂L/∂x of present nodes only): 64-wide column blocks up to the
-    // larger extent (SG_WEB_HEAD_TRIM=0: all Dp / 64)
-    const int ncp = SG_WEB_HEAD_TRIM ? min(nc, (max(ex.x, ex.y) + 63) >> 6) : nc;
+    // larger extent
+    const int ncp = min(nc, (max(ex.x, ex.y) + 63) >> 6);
     const float *x1 = A.X + p * Dp, *x2 = A.X + (A.Cp + p) * Dp;
     const float *Tp = A.T + (size_t)p * K * Dp;
     float m[WKP];
@@ -2335,7 +1958,7 @@ static int gcn_launch(bool bwd, const WebPlan &W, const GcnArgs &A, int64_t n_in
     // forward blocks per CU: 2 of the 3 that the LDS admits (4.445 vs 4.32 M pairs/s on C5,
     // profiles/r03_c5ab/knob_*: fewer blocks contend for the CU's LDS and issue slots, and
     // leave room for the pipelined GEMMs); SG_WEB_FWD_BPC=n sets it (A/B)
-    int want = SG_WEB_FWD_BPC_DEF;
+    int want = 2;
     const char *e = getenv("SG_WEB_FWD_BPC");
     if (e && atoi(e) > 0) want = atoi(e);
     if (want < per_cu) per_cu = want;
@@ -2382,46 +2005,61 @@ int sg_web_lds_ok(const sg_model_t *m) {
 // instance kernel done, G[slot] = the GEMMs of the chunk in that workspace slot done), one
 // set per (device, caller stream): calls on different caller streams do not share a second
 // stream (no false dependency between them), and calls from any host thread on the same
-// caller stream reuse one set.  The registry is a small LRU (kWebAuxMax sets): a caller
-// that churns through short-lived streams recycles the least recently used set (after its
-// second stream drains) instead of growing the list.  A caller stream whose handle is
-// reused after it was destroyed inherits that set, which is harmless: the set only orders
-// the call's own work.  sg_web_release() destroys them all (teardown).
+// caller stream reuse one set.  A set is leased for the whole sg_web_run call (in_use): the
+// registry keeps up to kWebAuxMax sets, and a caller stream without a set recycles the least
+// recently used set of its device only when no call holds it (else a new set is created),
+// so no call can see its stream and events handed to another caller between its event
+// record and the matching wait.  The recycled set's second stream is drained after the
+// registry lock is released.  A caller stream whose handle is reused after it was destroyed
+// inherits that set, which is harmless: the set only orders the call's own work.
+// sg_web_release() destroys them all (teardown, no call in flight).
 struct WebAux {
   int dev;
   hipStream_t caller, aux;
   hipEvent_t ev[3];
   uint64_t last_use;
+  int in_use;
 };
 constexpr size_t kWebAuxMax = 16;
 static std::mutex g_web_aux_mu;
-static std::vector<WebAux> g_web_aux;
+static std::list<WebAux> g_web_aux;   // stable addresses: leases point into it
 static uint64_t g_web_aux_tick = 0;
 
-static int web_aux(hipStream_t caller, hipStream_t *gs, hipEvent_t *evF, hipEvent_t *evG) {
+// releases the set at the end of the call that leased it
+struct WebAuxLease {
+  WebAux *a = nullptr;
+  ~WebAuxLease() {
+    if (a) {
+      std::lock_guard<std::mutex> lk(g_web_aux_mu);
+      --a->in_use;
+    }
+  }
+};
+
+static int web_aux(hipStream_t caller, WebAuxLease *lease, hipStream_t *gs, hipEvent_t *evF,
+                   hipEvent_t *evG) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return SG_ERR_HIP;
-  std::lock_guard<std::mutex> lk(g_web_aux_mu);
   WebAux *a = nullptr;
-  for (WebAux &x : g_web_aux)
-    if (x.dev == dev && x.caller == caller) a = &x;
-  if (!a) {
-    WebAux x;
-    x.dev = dev;
-    x.caller = caller;
-    x.last_use = 0;
-    if (g_web_aux.size() >= kWebAuxMax) {
-      // recycle the least recently used set of this device (its queued work first)
-      WebAux *lru = nullptr;
+  bool drain = false;
+  {
+    std::lock_guard<std::mutex> lk(g_web_aux_mu);
+    for (WebAux &x : g_web_aux)
+      if (x.dev == dev && x.caller == caller) a = &x;
+    if (!a && g_web_aux.size() >= kWebAuxMax) {
+      // recycle the least recently used idle set of this device
       for (WebAux &y : g_web_aux)
-        if (y.dev == dev && (!lru || y.last_use < lru->last_use)) lru = &y;
-      if (lru) {
-        if (hipStreamSynchronize(lru->aux) != hipSuccess) return SG_ERR_HIP;
-        lru->caller = caller;
-        a = lru;
+        if (y.dev == dev && y.in_use == 0 && (!a || y.last_use < a->last_use)) a = &y;
+      if (a) {
+        a->caller = caller;
+        drain = true;
       }
     }
     if (!a) {
+      WebAux x;
+      x.dev = dev;
+      x.caller = caller;
+      x.in_use = 0;
       for (int e = 0; e < 3; ++e)
         if (hipEventCreateWithFlags(&x.ev[e], hipEventDisableTiming) != hipSuccess)
           return SG_ERR_HIP;
@@ -2430,8 +2068,13 @@ static int web_aux(hipStream_t caller, hipStream_t *gs, hipEvent_t *evF, hipEven
       g_web_aux.push_back(x);
       a = &g_web_aux.back();
     }
+    a->last_use = ++g_web_aux_tick;
+    ++a->in_use;
+    lease->a = a;
   }
-  a->last_use = ++g_web_aux_tick;
+  // the recycled set's earlier work (another caller's) is done before this call reuses it;
+  // the lease keeps any other caller off the set meanwhile
+  if (drain && hipStreamSynchronize(a->aux) != hipSuccess) return SG_ERR_HIP;
   *gs = a->aux;
   *evF = a->ev[0];
   evG[0] = a->ev[1];
@@ -2540,8 +2183,9 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
   hipStream_t gs = st;
   hipEvent_t evF = nullptr, evG[2] = {nullptr, nullptr};
   const int64_t nch = n_pairs > 0 ? (n_pairs + chunk - 1) / chunk : 0;
+  WebAuxLease lease;   // held until this call has enqueued all of its work
   if (pipe_env && nch > 1) {
-    if (web_aux(st, &gs, &evF, evG) != SG_OK) return SG_ERR_HIP;
+    if (web_aux(st, &lease, &gs, &evF, evG) != SG_OK) return SG_ERR_HIP;
   }
   const bool pipe = gs != st;
   struct Slot {
@@ -2573,8 +2217,8 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     g.icls = units ? S.icls : nullptr;
     g.X = S.X;
     // the forward's dropout bits for the backward (training calls)
-    g.masks = (bwd && SG_WEB_MASKS) ? S.MASK : nullptr;
-    g.d2 = (bwd && SG_WEB_D2) ? S.D2 : nullptr;
+    g.masks = bwd ? S.MASK : nullptr;
+    g.d2 = bwd ? S.D2 : nullptr;
     g.GX = S.GX;
     g.n_pairs = n;
     g.pair_offset = pair_offset + c0;
@@ -2609,17 +2253,14 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     float *X = S.X, *GX = S.GX, *T = S.T, *GM = S.GM;
     // SG_WEB_TKG=0: web_t_kernel_b3, one k per block (read per call: a test compares the two)
     const char *tkg_e = getenv("SG_WEB_TKG");
-    const bool tkg = SG_WEB_TKG && !(tkg_e && tkg_e[0] == '0');
-    if (SG_WEB_T_BF3 && tkg)
+    const bool tkg = !(tkg_e && tkg_e[0] == '0');
+    if (tkg)
       hipLaunchKernelGGL(web_t_kernel_kg, dim3((unsigned)nblk, Dp / TB, (K + TKG - 1) / TKG),
                          dim3(512), 0, gs, X + ws.Cp * Dp, Wg, S.EXT128, n, Dp, K, T, X);
-    else if (SG_WEB_T_BF3)
+    else
       hipLaunchKernelGGL(web_t_kernel_b3<true>, web_pb_grid(nblk, Dp / TB, K), dim3(256),
                          web_lds_pad("SG_WEB_TPAD", (const void *)web_t_kernel_b3<true>), gs,
                          X + ws.Cp * Dp, Wg, S.EXT128, n, Dp, K, T, X);
-    else
-      hipLaunchKernelGGL(web_t_kernel, dim3((unsigned)nblk, Dp / TB, K), dim3(256), 0, gs,
-                         X + ws.Cp * Dp, Wg, S.EXT128, n, Dp, K, T);
     HeadArgs h = H;
     h.X = X; h.T = T; h.ext = S.EXT; h.ext128 = S.EXT128; h.GX = GX; h.GM = GM;
     h.n = n;
@@ -2627,32 +2268,19 @@ int sg_web_run(const sg_model_t *m, const sg_csr_store_t *store, const int32_t *
     h.s_out = s_out ? s_out + c0 : nullptr;
     const int hb = (int)((n + 3) / 4 < ws.head_blocks ? (n + 3) / 4 : ws.head_blocks);
     if (bwd) {
-      if (SG_WEB_T_BF3) {
-        hipLaunchKernelGGL((web_head_kernel<true, true>), dim3(hb), dim3(256), head_lds, gs, h);
-        hipLaunchKernelGGL(web_gx1_kernel_b3, web_pb_grid(nblk, Dp / TB, 1), dim3(256),
-                           web_lds_pad("SG_WEB_GXPAD", (const void *)web_gx1_kernel_b3), gs,
-                           X + ws.Cp * Dp, GM, Wg, S.EXT128, n, Dp, K, GX);
-        hipLaunchKernelGGL(web_gx2_kernel_b3, web_pb_grid(nblk, Dp / TB, 1), dim3(256),
-                           web_lds_pad("SG_WEB_GXPAD", (const void *)web_gx2_kernel_b3), gs, X,
-                           GM, Wh, S.EXT128, n, Dp, K, GX + ws.Cp * Dp);
-        // gV rides along
-        hipLaunchKernelGGL(web_wgrad_kernel_b3, dim3((Dp / TB) * (Dp / TB), K, WSPLIT), dim3(256),
-                           web_lds_pad("SG_WEB_WGPAD", (const void *)web_wgrad_kernel_b3), gs, X,
-                           X + ws.Cp * Dp, GM, S.EXT16, n, Dp, K, GWS, GVS);
-      } else {
-        hipLaunchKernelGGL((web_head_kernel<true, false>), dim3(hb), dim3(256), head_lds, gs, h);
-        hipLaunchKernelGGL(web_gx2_kernel, dim3((unsigned)nblk, Dp / TB), dim3(256), 0, gs, X, GM,
-                           Wh, S.EXT128, n, Dp, K, GX + ws.Cp * Dp);
-        hipLaunchKernelGGL(web_wgrad_kernel, dim3((Dp / TB) * (Dp / TB), K, WSPLIT), dim3(256), 0,
-                           gs, X, X + ws.Cp * Dp, GM, S.EXT16, n, Dp, K, GWS);
-        hipLaunchKernelGGL(web_gv_kernel, dim3(2 * Dp / 64, WSPLIT), dim3(256), 0, gs, X, GM, n,
-                           ws.Cp, Dp, K, GVS);
-      }
+      hipLaunchKernelGGL((web_head_kernel<true, true>), dim3(hb), dim3(256), head_lds, gs, h);
+      hipLaunchKernelGGL(web_gx1_kernel_b3, web_pb_grid(nblk, Dp / TB, 1), dim3(256),
+                         web_lds_pad("SG_WEB_GXPAD", (const void *)web_gx1_kernel_b3), gs,
+                         X + ws.Cp * Dp, GM, Wg, S.EXT128, n, Dp, K, GX);
+      hipLaunchKernelGGL(web_gx2_kernel_b3, web_pb_grid(nblk, Dp / TB, 1), dim3(256),
+                         web_lds_pad("SG_WEB_GXPAD", (const void *)web_gx2_kernel_b3), gs, X,
+                         GM, Wh, S.EXT128, n, Dp, K, GX + ws.Cp * Dp);
+      // gV rides along
+      hipLaunchKernelGGL(web_wgrad_kernel_b3, dim3((Dp / TB) * (Dp / TB), K, WSPLIT), dim3(256),
+                         web_lds_pad("SG_WEB_WGPAD", (const void *)web_wgrad_kernel_b3), gs, X,
+                         X + ws.Cp * Dp, GM, S.EXT16, n, Dp, K, GWS, GVS);
     } else {
-      if (SG_WEB_T_BF3)
-        hipLaunchKernelGGL((web_head_kernel<false, true>), dim3(hb), dim3(256), head_lds, gs, h);
-      else
-        hipLaunchKernelGGL((web_head_kernel<false, false>), dim3(hb), dim3(256), head_lds, gs, h);
+      hipLaunchKernelGGL((web_head_kernel<false, true>), dim3(hb), dim3(256), head_lds, gs, h);
     }
   };
   // chunk c's backward instance kernel (stream st)

@@ -827,6 +827,9 @@ static int32_t fwd_bwd_impl(const sg_model_t *model, const void *records, const 
   const int C = c.plan.n_params + 1;
   float *slab = (float *)workspace;
   if (adam && n_pairs == 0) return SG_ERR_ARG;   // (no update from an empty batch)
+  // one-call Adam covers up to 65,536 parameters (the fused reduction's columns, or
+  // sg_adam_tf's single workgroup); larger models call sg_fwd_bwd_* + sg_adam_tf_ex
+  if (adam && C - 1 > 65536) return SG_ERR_UNSUPPORTED;
   if (n_pairs == 0) {
     if (hipMemsetAsync(grad_out, 0, (size_t)c.plan.n_params * 4u, st) != hipSuccess)
       return SG_ERR_HIP;
@@ -837,7 +840,7 @@ static int32_t fwd_bwd_impl(const sg_model_t *model, const void *records, const 
   // sg_train_step: the fused path's gradient reduction applies Adam in the same launch
   // (sg_reduce_adam) with the step scalars the fused kernel's block 0 leaves in the
   // reduction's partial rows (unused by the one-pass reduction)
-  const bool fuse_adam = adam && c.path == 1 && C - 1 <= 65536;
+  const bool fuse_adam = adam && c.path == 1;
   float *adam_pre = slab + ntn_offset_floats(c, n_pairs) - (int64_t)kReduceStrands * C;
   SgAdamPre pre_args;
   if (fuse_adam) {

@@ -523,6 +523,11 @@ class GraphSteps(object):
         import torch
         if model.kernel_path != 1:
             raise RuntimeError('graph-captured steps need the fused path (kernel path 1)')
+        if model.grad_hook is not None:
+            # a data-parallel hook is host-driven (torch.distributed / gloo): it cannot be
+            # recorded into a hipGraph, and a replay would silently skip the exchange
+            raise RuntimeError('graph-captured steps do not support a grad_hook (the '
+                               'all-reduce of a sharded step); run eager train_step instead')
         self.model, self.feed, self.n_steps = model, feed, int(n_steps)
         m = model
         self.seed_dev = torch.tensor([m._seed(None)], dtype=torch.int64, device=m.device)
@@ -546,7 +551,7 @@ class GraphSteps(object):
     def _body(self, ws):
         m = self.model
         b = self.feed.next_batch()
-        if m.grad_hook is None and m._adam_ws is None:   # reduction + Adam in one launch
+        if m._adam_ws is None:   # reduction + Adam in one launch
             f = m.flags
             _lib.train_step_dseed(m.sg, b.records, b.n_pairs, b.pair_offset, b.batch_total,
                                   m.params, self.seed_dev, b.y_stats, 1, None, m.grad,
@@ -556,8 +561,6 @@ class GraphSteps(object):
             _lib.fwd_bwd_dseed(m.sg, b.records, b.n_pairs, b.pair_offset, b.batch_total,
                                m.params, self.seed_dev, b.y_stats, 1, None, m.grad, m.loss_buf,
                                ws)
-            if m.grad_hook is not None:
-                m.grad_hook(m)
             m.apply_adam()
         _lib.seed_advance(self.seed_dev, 1)
 

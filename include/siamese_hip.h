@@ -414,8 +414,9 @@ int32_t sg_adam_tf_ex(float *params, float *m, float *v, const float *grad, int6
  * launch; other paths run the two calls.  params, grad_out, loss_out, m, v and
  * beta_powers end as after sg_fwd_bwd_cls + sg_adam_tf, bitwise; reg_loss_out holds the
  * same wd·½Σθ² summed in another order (double partials).  A multi-GPU step, whose
- * gradient is all-reduced between the two, keeps the separate calls.  Replaces the
- * train op of models.py:28-36 (AdamOptimizer(lr).minimize(loss)).
+ * gradient is all-reduced between the two, keeps the separate calls.  Models of more than
+ * 65,536 parameters return SG_ERR_UNSUPPORTED (call sg_fwd_bwd_* + sg_adam_tf_ex).
+ * Replaces the train op of models.py:28-36 (AdamOptimizer(lr).minimize(loss)).
  */
 typedef struct sg_adam_args {
   float *m, *v;            /* device [n_params] moments */
