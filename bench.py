@@ -79,6 +79,11 @@ def parse():
     p.add_argument('--json-out', default='')
     p.add_argument('--emulate-world', type=int, default=0,
                    help='diagnostic: time rank 0\'s share of a W-GPU step on one GPU (no collective)')
+    p.add_argument('--emulate-collective', action='store_true',
+                   help='with --emulate-world: step as a real rank does (fused kernel, gradient '
+                        'reduction, ncclAllReduce of the flat gradient on a world-size-1 RCCL '
+                        'communicator on the compute stream, Adam launch), so the collective\'s '
+                        'launch cost is in the timed step (its data path is a 1-rank no-op)')
     return p.parse_args()
 
 
@@ -269,6 +274,11 @@ def main():
                                            batch_total=shard.total, y_stats=batch.y_stats)
             batch = model.balance(batch) if balance else batch
     hook, collective = None, None
+    if ew and args.emulate_collective:
+        from graphembedding_amd.rccl import RcclComm
+        from graphembedding_amd.shard import make_rccl_hook
+        comm = RcclComm(0, 1, store=dist.HashStore())
+        hook, collective = make_rccl_hook(comm), 'rccl'
     if world > 1:
         # RCCL on the compute stream, in order with the fused kernels (no side stream, no
         # cross-stream events: 8 us less per step than torch.distributed's RCCL call,
@@ -539,9 +549,9 @@ def main():
         if args.json_out:
             with open(args.json_out, 'w') as f:
                 f.write(line + '\n')
+    if collective == 'rccl':
+        comm.destroy()
     if world > 1:
-        if collective == 'rccl':
-            comm.destroy()
         dist.destroy_process_group()
 
 

@@ -117,8 +117,13 @@ __device__ __forceinline__ float row_sum16(float v) {
 // row_sum16 of N independent values, step-interleaved: a DPP read of a VGPR written by
 // the previous VALU instruction needs two wait states (s_nop 1 in a lone chain); with
 // N >= 3 chains advanced in lockstep the other chains' adds fill them
+// (the inputs are made opaque first: a product x = a·b would otherwise be folded into the
+// first step as fma(a, b, dpp(x)), a v_mov_b32_dpp + v_fmac_f32 instead of one
+// v_add_f32_dpp)
 template <int N>
 __device__ __forceinline__ void row_sum16_n(float (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm("" : "+v"(v[i]));
 #pragma unroll
   for (int i = 0; i < N; ++i) v[i] += dpp<0xB1>(v[i]);
 #pragma unroll
@@ -128,6 +133,5 @@ __device__ __forceinline__ void row_sum16_n(float (&v)[N]) {
 #pragma unroll
   for (int i = 0; i < N; ++i) v[i] += dpp<0x140>(v[i]);
 }
-
 
 }  // namespace sgk

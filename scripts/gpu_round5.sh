@@ -38,6 +38,7 @@ for rep in 1 2; do
       emu8) BENCH_ARGS_AB="--emulate-world 8 --steps 300 --warmup 30" ;;
       n1sep) BENCH_ARGS_AB="--steps 40 --warmup 5 --no-fused-adam" ;;
       emu8sep) BENCH_ARGS_AB="--emulate-world 8 --steps 300 --warmup 30 --no-fused-adam" ;;
+      emu8c) BENCH_ARGS_AB="--emulate-world 8 --emulate-collective --steps 300 --warmup 30" ;;
       n1ea) BENCH_ARGS_AB="--steps 40 --warmup 5 --events after" ;;
       emu8ea) BENCH_ARGS_AB="--emulate-world 8 --steps 300 --warmup 30 --events after" ;;
       c4) BENCH_ARGS_AB="--dataset syn_aids10knef --steps 2 --warmup 1" ;;
