@@ -42,3 +42,23 @@ def test_graph_steps_equal_eager_steps(gpu, stack):
         assert torch.equal(a, b)
     assert not torch.equal(m_g.params, torch.from_numpy(
         np.asarray(m_g.flat_params())).to(gpu) * 0), 'params moved'
+
+
+def test_graph_capture_refuses_a_grad_hook(gpu):
+    """A data-parallel gradient hook is host-driven (torch.distributed): a hipGraph cannot
+    record it, so capture_train_steps refuses a model that has one instead of silently
+    replaying steps without the exchange."""
+    from graphembedding_amd.config import Flags
+    from graphembedding_amd.data import synthetic_ged_matrix
+    from graphembedding_amd.data_siamese import SiameseModelData
+    from graphembedding_amd.device_sampler import DeviceFeed
+    from graphembedding_amd.dist_calculator import DistCalculator
+    from graphembedding_amd.model_mse import SiameseGCNTNMSE
+    f = Flags(dataset='syn_aids80nef', node_feat_order='sorted')
+    data = SiameseModelData(f)
+    gs = list(data.orig_train_graphs) + [data.test_data.gs[i].nxgraph for i in range(data.m)]
+    dc = DistCalculator.from_matrix(f.dataset, gs, synthetic_ged_matrix(gs))
+    model = SiameseGCNTNMSE(data.input_dim(), f, device=gpu)
+    model.grad_hook = lambda m: None
+    with pytest.raises(RuntimeError, match='grad_hook'):
+        model.capture_train_steps(DeviceFeed(model, data, dc, 'train'), n_steps=2)
