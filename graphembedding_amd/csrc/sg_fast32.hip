@@ -901,70 +901,104 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
 // ---- NTN gradients: O[a][b'][k] = Σ_p gm_p[k] x1_p[a] x2_p[b'], a, b' <= D ----
 // with x1_p[D] = x2_p[D] = 1: gW = O[a < D][b' < D], gV[k][a] = O[a][D],
 // gV[k][D + b'] = O[D][b'], gb = O[D][D].  Workgroup b sums its contiguous share
-// of the pairs with MFMA: output rows a (two 16-row tiles), columns c = b'·K + k
-// (20 tiles of 16, 4 waves × 5), the pairs are the K dimension (4 per k-step),
-// operands from an LDS-staged chunk.  The result goes to the NTN columns of slab
-// row b (the fused kernel writes the other columns of the same row).
+// of the pairs with MFMA: output rows a (16-row tiles), columns c = b'·K + k (the
+// ceil((D + 1) K / 16) column tiles, NTW per wave, dealt round-robin over the NWV waves),
+// the pairs are the K dimension (4 per k-step), operands from an LDS-staged chunk whose
+// successor is loaded into registers meanwhile.  The result goes to the NTN columns of slab
+// row b (the fused kernel writes the other columns of the same row).  ROW1: a second row
+// tile (D > 16, rows 16..D); at D = 16 (the Average / Attention stacks) its one live row
+// a = 16 is x1's constant 1, so O[16][c] = Σ_p gm_p[k] x2_p[b'] is a column sum, kept on
+// VALU per lane and summed over the four row groups at the end.  Round 6 (Average stack,
+// 490,000 pairs): 188 µs per launch with 20 column tiles x 2 row tiles at any D and one
+// global round trip per 64-pair chunk, 131 µs with D's tiles only, 70 µs double-buffered,
+// 62 µs at 8 waves (profiles/r06_e, r06_f).
 constexpr int WG_CHUNK = 64;   // pairs staged per LDS round
 
-__global__ void __launch_bounds__(256) sg_ntn_wgrad_kernel(const float *__restrict__ ntn,
+template <int NTW, bool ROW1, int NWV>
+__global__ void __launch_bounds__(64 * NWV) sg_ntn_wgrad_kernel(const float *__restrict__ ntn,
                                                           int64_t n_pairs, int D, int oW,
                                                           int oV, int obn, int C,
                                                           float *__restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) float st[WG_CHUNK * NBUF];
+  constexpr int CH = WG_CHUNK * NWV / 4, NT = 64 * NWV;   // pairs per chunk, threads
+  __shared__ __attribute__((aligned(16))) float st[CH * NBUF];
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   const int g = l >> 4, j = l & 15;
   const int nb = gridDim.x;
   const int64_t p0 = n_pairs * blockIdx.x / nb, p1 = n_pairs * (blockIdx.x + 1) / nb;
   const int DK = (D + 1) * FK;   // columns b' <= D
-  // this lane's columns in its wave's 5 column tiles
-  int cb_[5], ck_[5];
+  // this lane's columns in its wave's NTW column tiles (tiles past DK read gm slot 15,
+  // which is 0: their products are zero and they are not written)
+  int cb_[NTW], ck_[NTW];
 #pragma unroll
-  for (int t = 0; t < 5; ++t) {
-    const int c = 16 * (w + 4 * t) + j;
+  for (int t = 0; t < NTW; ++t) {
+    const int c = 16 * (w + NWV * t) + j;
     const int cc = c < DK ? c : 0;
     cb_[t] = NC + cc / FK;          // x2[b'] offset in the pair's buffer row
     ck_[t] = c < DK ? 2 * NC + cc % FK : 2 * NC + 15;   // gm[k] (slot 15 is 0: k < FK only)
   }
-  f4 acc[2][5];
+  f4 acc[2][NTW];
+  float csum[NTW];   // !ROW1: Σ of this lane's pairs' products, column 16 (w + 4t) + j
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
+  for (int t = 0; t < NTW; ++t) {
+    acc[0][t] = acc[1][t] = f4{0.f, 0.f, 0.f, 0.f};
+    csum[t] = 0.f;
+  }
+  // the chunks are double-buffered through registers: chunk i + 1's loads are in flight
+  // while chunk i is multiplied out of LDS (one global round trip per chunk otherwise,
+  // ≈30 of them per block, each exposed)
+  constexpr int PER = CH * NBUF / 4 / NT;   // f4 per thread per chunk
+  static_assert(PER * NT * 4 == CH * NBUF, "chunk split");
+  f4 nx[PER];
+  auto fetch = [&](int64_t c0) __attribute__((always_inline)) {
+    const int np = (int)((p1 - c0) < CH ? (p1 - c0) : CH);
 #pragma unroll
-    for (int t = 0; t < 5; ++t) acc[rt][t] = f4{0.f, 0.f, 0.f, 0.f};
-  for (int64_t c0 = p0; c0 < p1; c0 += WG_CHUNK) {
-    const int np = (int)((p1 - c0) < WG_CHUNK ? (p1 - c0) : WG_CHUNK);
-    __syncthreads();
-    for (int i = tid; i < WG_CHUNK * NBUF / 4; i += 256) {
-      const int pp = i / (NBUF / 4);
-      ((f4 *)st)[i] = pp < np ? ((const f4 *)(ntn + (size_t)c0 * NBUF))[i] : f4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < PER; ++u) {
+      const int i = tid + NT * u, pp = i / (NBUF / 4);
+      nx[u] = pp < np ? ((const f4 *)(ntn + (size_t)c0 * NBUF))[i] : f4{0.f, 0.f, 0.f, 0.f};
     }
+  };
+  if (p0 < p1) fetch(p0);
+  for (int64_t c0 = p0; c0 < p1; c0 += CH) {
+    const int np = (int)((p1 - c0) < CH ? (p1 - c0) : CH);
+    __syncthreads();   // the previous chunk's reads are done
+#pragma unroll
+    for (int u = 0; u < PER; ++u) ((f4 *)st)[tid + NT * u] = nx[u];
     __syncthreads();
+    if (c0 + CH < p1) fetch(c0 + CH);
+#pragma unroll 2
     for (int k0 = 0; k0 < np; k0 += 4) {
       const float *row = st + (k0 + g) * NBUF;   // pair k0 + g (zero rows past np)
-      const float a0 = row[j], a1 = row[16 + j];
+      const float a0 = row[j];
+      const float a1 = ROW1 ? row[16 + j] : 0.f;
 #pragma unroll
-      for (int t = 0; t < 5; ++t) {
+      for (int t = 0; t < NTW; ++t) {
         const float bv = row[ck_[t]] * row[cb_[t]];
         acc[0][t] = mfma4(a0, bv, acc[0][t]);
-        acc[1][t] = mfma4(a1, bv, acc[1][t]);
+        if (ROW1) acc[1][t] = mfma4(a1, bv, acc[1][t]);
+        else csum[t] += bv;
       }
     }
+  }
+  if (!ROW1) {   // row a = D = 16: the column sums over the four row groups
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) csum[t] = xsum32(xsum16(csum[t]));
   }
   float *dst = slab + (size_t)blockIdx.x * C;
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-    for (int t = 0; t < 5; ++t) {
-      const int c = 16 * (w + 4 * t) + j;
+    for (int t = 0; t < NTW; ++t) {
+      const int c = 16 * (w + NWV * t) + j;
       const int bb = c / FK, k = c - bb * FK;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int a = 16 * rt + 4 * g + r;
         if (a > D || c >= DK) continue;
+        if (!ROW1 && rt == 1 && (g != 0 || r != 0)) continue;   // a = 16 only, from csum
         int prm_i;
         if (a < D) prm_i = bb < D ? oW + (a * D + bb) * FK + k : oV + k * 2 * D + a;
         else prm_i = bb < D ? oV + k * 2 * D + D + bb : obn + k;
-        dst[prm_i] = acc[rt][t][r];
+        dst[prm_i] = (!ROW1 && rt == 1) ? csum[t] : acc[rt][t][r];
       }
     }
 }
@@ -1034,8 +1068,15 @@ int64_t sg_fast32_ntn_floats(int64_t n_pairs) { return n_pairs * NBUF; }
 int sg_ntn_wgrad_run(const float *ntn, int64_t n_pairs, int D, int oW, int oV, int obn, int C,
                      float *slab, int blocks, hipStream_t st) {
   if (D < 1 || D > 31 || obn < 0) return SG_ERR_ARG;
-  hipLaunchKernelGGL(sg_ntn_wgrad_kernel, dim3(blocks), dim3(256), 0, st, ntn, n_pairs, D, oW, oV,
-                     obn, C, slab);
+  // column tiles per wave: ceil(ceil((D + 1) K / 16) / 4)
+  const int nct = ((D + 1) * FK + 15) / 16, ntw = (nct + 3) / 4;
+  // D <= 15: rows a <= D fit the first tile; D = 16 (the Average stack): row a = 16 on VALU
+  if (D <= 16 && nct <= 16)   // 8 waves of 2 tiles
+    hipLaunchKernelGGL((sg_ntn_wgrad_kernel<2, false, 8>), dim3(blocks), dim3(512), 0, st, ntn,
+                       n_pairs, D, oW, oV, obn, C, slab);
+  else
+    hipLaunchKernelGGL((sg_ntn_wgrad_kernel<5, true, 4>), dim3(blocks), dim3(256), 0, st, ntn,
+                       n_pairs, D, oW, oV, obn, C, slab);
   return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
 }
 
@@ -1126,9 +1167,9 @@ int sg_fast32_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void 
   }
 #undef SG32_LAUNCH
   if (bwd) {
-    hipLaunchKernelGGL(sg_ntn_wgrad_kernel, dim3(c.blocks), dim3(256), 0, stream,
-                       (const float *)ntn, n_pairs, P.D, P.offW, P.offV, P.offB, P.n_params + 1,
-                       slab);
+    const int rc = sg_ntn_wgrad_run((const float *)ntn, n_pairs, P.D, P.offW, P.offV, P.offB,
+                                    P.n_params + 1, slab, c.blocks, stream);
+    if (rc != SG_OK) return rc;
   }
   if (blocks_out) *blocks_out = c.blocks;
   return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
