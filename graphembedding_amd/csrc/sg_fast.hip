@@ -1023,14 +1023,18 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         gUa += INTENDED ? gs * rk : gs * rsum;
       }
       if constexpr (AVG) {
-        // this pair's row of the NTN-gradient buffer: x1|1 | x2|1 | gm (lane k = j of
-        // row group 0 holds gm_k)
+        // this pair's row of the NTN-gradient buffer: x1|1 | x2|1 | gm.  Two stores by
+        // every lane, no branch: lanes 0-31 write x1|1, lanes 32-63 x2|1, and the four row
+        // groups write the same gm_k (gmk is equal on the lanes of one k).  A store behind a
+        // branch made the loop's wait for the next record's prefetch a vmcnt(0), which
+        // also waited for this pair's stores (their HBM latency, every pair).
         float *nb_ = A.ntn + (size_t)(uint32_t)pcur * 80u;
-        if (l < 32) {
-          nb_[l] = l < DN ? sX[l] : (l == DN ? 1.f : 0.f);
-          nb_[32 + l] = l < DN ? sX[XO2 + l] : (l == DN ? 1.f : 0.f);
+        {
+          const int li = l & 31;
+          const float xv = sX[(l < 32 ? 0 : XO2) + (li < DN ? li : 47)];   // sX[47] = 0
+          nb_[l] = li < DN ? xv : (li == DN ? 1.f : 0.f);
+          nb_[64 + j] = j < FK ? gmk : 0.f;
         }
-        if (l < 16) nb_[64 + l] = l < FK ? gmk : 0.f;
       }
       const float gmk4 = gmk * A.ik4;
       float ge[2][RN];   // dL/dx · ik4 (before the x > 0 mask)
