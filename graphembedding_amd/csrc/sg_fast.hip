@@ -251,6 +251,24 @@ __device__ __forceinline__ float sg_sigmoid(float z) {
   return __builtin_amdgcn_rcpf(1.f + __expf(-z));
 }
 
+// xsum32(xsum16(a)) and xsum32(xsum16(b)) at once, bitwise the same sums ((x0 + x1) +
+// (x2 + x3) over the four rows of 16 lanes): v_permlane16_swap(a, b) leaves [a0, b0, a2, b2]
+// and [a1, b1, a3, b3], one add gives [a01, b01, a23, b23]; a permlane32 swap and an add
+// give [a, b, a, b], and a last permlane16 swap spreads a and b to every lane.  7 VALU
+// (two of them register copies) for what two separate reductions do in 12.
+__device__ __forceinline__ void xsum_pair(float &a, float &b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false,
+                                                  false);
+  const float s = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false,
+                                                  false);
+  const float t = __uint_as_float(q[0]) + __uint_as_float(q[1]);
+  const auto z = __builtin_amdgcn_permlane16_swap(__float_as_uint(t), __float_as_uint(t), false,
+                                                  false);
+  a = __uint_as_float(z[0]);
+  b = __uint_as_float(z[1]);
+}
+
 #ifdef SG_FAST_TIMING
 // Diagnostic build only (scripts/fast_timing.py): per-wave s_memrealtime stamps
 // (100 MHz) at start / after the prologue / after the pair loop / at the end,
@@ -848,15 +866,17 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         // Wa), att_n = sigmoid(H2[n] · h), e = Σ_n att_n H2[n]; x_s[j] = keep · e_j · ik4.
         // Lane (g, j) holds H2 rows 4r + g at feature j; absent rows (b1) are masked.
         float *sTmp = W + L::TMP;
+        float part[2] = {0.f, 0.f};
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const int KS = s2 ? K1 : K0, Ns = s2 ? N1 : N0;
-          float part = 0.f;
 #pragma unroll
-          for (int r = 0; r < KS; ++r) part += (4 * r + g < Ns) ? h2[s2][r] : 0.f;
-          const float e = xsum32(xsum16(part)) * (s2 ? invn1 : invn0);
-          if (g == 0) sTmp[16 * s2 + j] = e;
+          for (int r = 0; r < KS; ++r) part[s2] += (4 * r + g < Ns) ? h2[s2][r] : 0.f;
         }
+        xsum_pair(part[0], part[1]);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          if (g == 0) sTmp[16 * s2 + j] = part[s2] * (s2 ? invn1 : invn0);
         sg_wsync();
         float hp[2];   // row group g: the terms j' = 4g..4g+3 of (temp · Wa)[j]
 #pragma unroll
@@ -867,27 +887,31 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
             a = fmaf(sTmp[16 * s2 + 4 * g + i], sWat[(4 * g + i) * WAS + j], a);
           hp[s2] = a;
         }
+        xsum_pair(hp[0], hp[1]);
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) hA[s2] = sg_tanh(xsum32(xsum16(hp[s2])));
+        for (int s2 = 0; s2 < 2; ++s2) hA[s2] = sg_tanh(hp[s2]);
         float dd[K0 + K1];   // H2[n] · h: the node rows' sums, both sides interleaved
 #pragma unroll
         for (int r = 0; r < K0; ++r) dd[r] = h2[0][r] * hA[0];
 #pragma unroll
         for (int r = 0; r < K1; ++r) dd[K0 + r] = h2[1][r] * hA[1];
         row_sum16_n(dd);
+        float po[2] = {0.f, 0.f};
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const int KS = s2 ? K1 : K0, Ns = s2 ? N1 : N0;
-          float po = 0.f;
 #pragma unroll
           for (int r = 0; r < KS; ++r) {
             const float a = sg_sigmoid(dd[s2 * K0 + r]);
             att[s2][r] = a;
-            po += (4 * r + g < Ns) ? a * h2[s2][r] : 0.f;
+            po[s2] += (4 * r + g < Ns) ? a * h2[s2][r] : 0.f;
           }
-          const float e = xsum32(xsum16(po));
+        }
+        xsum_pair(po[0], po[1]);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
           const bool k4 = (m4 >> (16 * s2 + j)) & 1u;
-          if (g == 0) sX[XO2 * s2 + j] = k4 ? e * A.ik4 : 0.f;
+          if (g == 0) sX[XO2 * s2 + j] = k4 ? po[s2] * A.ik4 : 0.f;
         }
         sg_wsync();
 #pragma unroll
@@ -899,13 +923,17 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       } else if constexpr (AVG) {
         // x_s[j] = keep · mean over the side's nodes of H2[·][j] · ik4 (layers.py:136-140,
         // 287-288): lane (g, j) holds the rows of nodes 4r + g; absent rows hold b1
+        float part[2] = {0.f, 0.f};
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const int KS = s2 ? K1 : K0, Ns = s2 ? N1 : N0;
-          float part = 0.f;
 #pragma unroll
-          for (int r = 0; r < KS; ++r) part += (4 * r + g < Ns) ? h2[s2][r] : 0.f;
-          const float e = xsum32(xsum16(part)) * (s2 ? invn1 : invn0);
+          for (int r = 0; r < KS; ++r) part[s2] += (4 * r + g < Ns) ? h2[s2][r] : 0.f;
+        }
+        xsum_pair(part[0], part[1]);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const float e = part[s2] * (s2 ? invn1 : invn0);
           const bool k4 = (m4 >> (16 * s2 + j)) & 1u;
           if (g == 0) sX[XO2 * s2 + j] = k4 ? e * A.ik4 : 0.f;
         }
@@ -1000,7 +1028,10 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       const float rsum = row_sum16(rk);
       const float sv = INTENDED ? row_sum16(Uk * rk) : usum * rsum;
       if (!BWD) {
-        if (l == 0) A.s_out[pcur] = sv;
+        // every lane stores the (wave-uniform) score: a store behind a lane test is not
+        // counted on every path, and the loop's wait for the next record would become a
+        // vmcnt(0) that also waits for this store
+        A.s_out[pcur] = sv;
         return;
       }
       if (A.s_out && l == 0) A.s_out[pcur] = sv;
@@ -1121,9 +1152,10 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           }
         }
         float gu[2];
+        xsum_pair(ghp[0], ghp[1]);
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          const float gh = xsum32(xsum16(ghp[s2]));
+          const float gh = ghp[s2];
           gu[s2] = gh * (1.f - hA[s2] * hA[s2]);
           if (g == 0) sGU[16 * s2 + j] = gu[s2];
         }
@@ -1138,10 +1170,11 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
           for (int i = 0; i < 4; ++i) a = fmaf(sGU[16 * s2 + 4 * g + i], sWat[j * WAS + 4 * g + i], a);
           gtp[s2] = a;
         }
+        xsum_pair(gtp[0], gtp[1]);
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
           const int KS = s2 ? K1 : K0;
-          const float gt = xsum32(xsum16(gtp[s2])) * (s2 ? invn1 : invn0);
+          const float gt = gtp[s2] * (s2 ? invn1 : invn0);
 #pragma unroll
           for (int r = 0; r < KS; ++r)
             gxa[s2][r] = fmaf(att[s2][r], gej[s2], fmaf(gz[s2][r], hA[s2], gt));
