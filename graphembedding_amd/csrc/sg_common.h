@@ -119,7 +119,10 @@ __device__ __forceinline__ float sg_final_grad(int fa, float yeta, float s, floa
 // Wave-local LDS hand-off: every prior LDS access of this wave has landed and
 // the compiler may not move memory operations across.
 __device__ __forceinline__ void sg_wsync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // a wavefront-scope fence: orders this wave's LDS accesses in the compiler and emits no
+  // wait (a wave's DS operations are performed in program order; the compiler still waits
+  // for the values it reads)
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
 
