@@ -1568,16 +1568,38 @@ static FastCfg fast_cfg(const SgGenPlan &P, int64_t n_pairs, bool bwd) {
 
 struct ClassWeights {
   float w[4];
+  bool set;   // SG_CLS_W given: it applies to every stack
 };
 
 static ClassWeights class_weights_from_env() {
-  ClassWeights c = {{1.f, 1.315f, 1.316f, 1.493f}};
+  ClassWeights c = {{1.f, 1.f, 1.f, 1.f}, false};
   if (const char *ev = getenv("SG_CLS_W")) {
     float w[4];
-    if (sscanf(ev, "%f,%f,%f,%f", &w[0], &w[1], &w[2], &w[3]) == 4)
+    if (sscanf(ev, "%f,%f,%f,%f", &w[0], &w[1], &w[2], &w[3]) == 4) {
       for (int k = 0; k < 4; ++k) c.w[k] = w[k] > 0.f ? w[k] : 1.f;
+      c.set = true;
+    }
   }
   return c;
+}
+
+// Relative cost of a pair of class (N0 > 8) + 2 (N1 > 8) per stack: the median per-class
+// µs/pair of the per-wave timing build (scripts/fast_timing.py), N = 1 (W = 8 within 0.5%).
+// Round 6 (profiles/r06_p … r06_u): the default stack on f32 records 1 : 1.355 : 1.351 :
+// 1.546 (its pair body changed since round 4's 1 : 1.315 : 1.316 : 1.493, which left the
+// (2, 2) class's waves ending 23 µs early; C2 +0.7%, an emulated W = 8 rank −1.5%); on
+// bf16 records (C3) 1 : 1.307 : 1.316 : 1.497, where round 4's weights stay (larger or
+// smaller weights measured slower); Average 1 : 1.212 : 1.211 : 1.330 (+5.2%); Attention
+// (its kernel is in another translation unit, which the timing build does not read back) by
+// an A/B sweep, 1 : 1.18 : 1.18 : 1.28 (+6.6%).
+static void class_weights_for(bool avg, bool att, bool bf16, float *w) {
+  static const float kDefault[4] = {1.f, 1.355f, 1.351f, 1.546f};
+  static const float kBf16[4] = {1.f, 1.315f, 1.316f, 1.493f};
+  static const float kAverage[4] = {1.f, 1.212f, 1.211f, 1.330f};
+  static const float kAttention[4] = {1.f, 1.18f, 1.18f, 1.28f};
+  static const ClassWeights env = class_weights_from_env();   // parsed once per process
+  const float *src = env.set ? env.w : (att ? kAttention : (avg ? kAverage : (bf16 ? kBf16 : kDefault)));
+  for (int k = 0; k < 4; ++k) w[k] = src[k];
 }
 
 // Relative pair-loop speed of XCD x (block b on XCD b % 8), ×10^4.  The default is equal
@@ -1633,16 +1655,11 @@ static int fast_run_impl(const sg_model_t *m, const SgGenPlan &P, bool bwd, cons
     return SG_ERR_ARG;
   A.order = order;
   A.cls = order ? class_start : nullptr;
-  // relative cost of a pair of class (N0 > 8) + 2 (N1 > 8): the class-exclusive schedule
-  // gives each class waves in proportion to count x cost (SG_CLS_W="w0,w1,w2,w3" to tune)
-  // (measured per-class µs/pair, scripts/fast_timing.py: profiles/r04_tim 1, 1.315, 1.311, 1.488
-  // at N = 1 and 1, 1.315, 1.316, 1.493 at an emulated W = 8 rank; round 5's A/B
-  // (profiles/r05_c): an emulated W = 8 rank 0.1338 / 0.1335 ms against 0.1345 / 0.1340 with
-  // the round-3 weights 1, 1.29, 1.31, 1.47, N = 1 within the box's spread)
-  // (the environment is parsed once per process, and only for class-scheduled launches)
+  // the class-exclusive schedule gives each class waves in proportion to count x cost
+  // (class_weights_for; SG_CLS_W="w0,w1,w2,w3" to tune); the environment is parsed once
+  // per process, and only for class-scheduled launches
   if (A.cls) {
-    static const ClassWeights cwt = class_weights_from_env();
-    for (int k = 0; k < 4; ++k) A.cw[k] = cwt.w[k];
+    class_weights_for(plan_avg(P), plan_att(P), P.adj_dtype == SG_DTYPE_BF16, A.cw);
     static const XcdWeights xwt = xcd_weights_from_env();
     for (int k = 0; k < 8; ++k) A.xw[k] = xwt.w[k];
   } else {

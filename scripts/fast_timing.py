@@ -4,6 +4,7 @@ Build the timing variant here, then run on the box:
     python graphembedding_amd/build.py --out graphembedding_amd/lib/libsiamese_timing.so \
         -DSG_FAST_TIMING=1
     SG_LIB=graphembedding_amd/lib/libsiamese_timing.so python scripts/fast_timing.py 1 8
+        [--stack=average|attention] [--records=bf16]
 
 For each emulated world size W the script runs rank 0's shard of the bench workload
 (AIDS700nef all-pairs), then reads the per-wave s_memrealtime stamps (100 MHz): start,
@@ -38,15 +39,25 @@ def main():
         raise SystemExit('SG_LIB must point at a -DSG_FAST_TIMING=1 build')
     L.sg_fast_timing_fetch.argtypes = [ctypes.c_void_p, ctypes.c_int]
     device = torch.device('cuda', 0)
-    flags = Flags(dropout=0.1)
+    # --stack average|attention (the tuning.py stack), --records bf16 (config C3)
+    opt = {a.split('=')[0]: a.split('=')[1] for a in sys.argv[1:] if '=' in a}
+    fl = dict(dropout=0.1, record_dtype=opt.get('--records', 'f32'))
+    stack = opt.get('--stack', 'default')
+    if stack in ('average', 'attention'):
+        fl.update(num_layers=4,
+                  layer_2='Average' if stack == 'average' else 'Attention:input_dim=16',
+                  layer_3='NTN:input_dim=16,feature_map_dim=10,inneract=relu,dropout=True,'
+                          'bias=True')
+    flags = Flags(**fl)
     gs = load_graph_set('syn_aids700nef', n_max=10)
     labels = gs.label_matrix(flags.yeta)
     balance = '--batch-order' not in sys.argv
     worlds = [int(a) for a in sys.argv[1:] if not a.startswith('--')] or [1, 8]
+    print('stack:', stack, 'records:', fl['record_dtype'])
     print('order:', 'class' if balance else 'batch')
     for W in worlds:
         model = SiameseGCNTNMSE(gs.d_in, flags, device=device, n_max=gs.n_max)
-        shard = AllPairsShard(gs, labels, 0, W, device=device)
+        shard = AllPairsShard(gs, labels, 0, W, device=device, dtype=fl['record_dtype'])
         batch = shard.batch(model, balance=balance)
         model.workspace(batch.n_pairs)
         for _ in range(5):
