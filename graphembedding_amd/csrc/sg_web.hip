@@ -2087,17 +2087,21 @@ int sg_web_release_aux() {
   int rc = SG_OK;
   int cur = 0;
   const bool have_cur = hipGetDevice(&cur) == hipSuccess;
-  for (WebAux &x : g_web_aux) {
-    if (hipSetDevice(x.dev) != hipSuccess) {
-      rc = SG_ERR_HIP;
+  for (auto it = g_web_aux.begin(); it != g_web_aux.end();) {
+    WebAux &x = *it;
+    // a set leased by a call still in flight on another thread stays (its lease points at
+    // it); a later sg_web_release frees it
+    if (x.in_use > 0 || hipSetDevice(x.dev) != hipSuccess) {
+      if (x.in_use == 0) rc = SG_ERR_HIP;
+      ++it;
       continue;
     }
     // the second stream's work must be done before its objects go
     if (hipStreamSynchronize(x.aux) != hipSuccess) rc = SG_ERR_HIP;
     for (int e = 0; e < 3; ++e) (void)hipEventDestroy(x.ev[e]);
     if (hipStreamDestroy(x.aux) != hipSuccess) rc = SG_ERR_HIP;
+    it = g_web_aux.erase(it);
   }
-  g_web_aux.clear();
   if (have_cur) (void)hipSetDevice(cur);
   return rc;
 }
