@@ -1054,17 +1054,19 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
         gUa += INTENDED ? gs * rk : gs * rsum;
       }
       if constexpr (AVG) {
-        // this pair's row of the NTN-gradient buffer: x1|1 | x2|1 | gm.  Two stores by
-        // every lane, no branch: lanes 0-31 write x1|1, lanes 32-63 x2|1, and the four row
-        // groups write the same gm_k (gmk is equal on the lanes of one k).  A store behind a
-        // branch made the loop's wait for the next record's prefetch a vmcnt(0), which
-        // also waited for this pair's stores (their HBM latency, every pair).
-        float *nb_ = A.ntn + (size_t)(uint32_t)pcur * 80u;
+        // this pair's row of the NTN-gradient buffer, sg_ntn_wgrad's compact D = 16 layout
+        // (NBUF16, 48 floats): x1 | x2 | gm, zeros, the constant 1 in slot 47.  One store by
+        // every lane, no branch: lanes 0-31 write x1 | x2 (sX[0..31]), lanes 32-47 gm_k or
+        // the pad, and lanes 48-63 repeat lanes 32-47's stores (the four row groups hold the
+        // same gm_k).  A store behind a branch made the loop's wait for the next record's
+        // prefetch a vmcnt(0), which also waited for this pair's stores (their HBM latency,
+        // every pair).
+        static_assert(DN == 16 && XO2 == 16, "the compact row holds 16-element x1 and x2");
+        float *nb_ = A.ntn + (size_t)(uint32_t)pcur * 48u;
         {
-          const int li = l & 31;
-          const float xv = sX[(l < 32 ? 0 : XO2) + (li < DN ? li : 47)];   // sX[47] = 0
-          nb_[l] = li < DN ? xv : (li == DN ? 1.f : 0.f);
-          nb_[64 + j] = j < FK ? gmk : 0.f;
+          const float xv = sX[l & 31];
+          const float gv = j < FK ? gmk : (j == 15 ? 1.f : 0.f);
+          nb_[l < 48 ? l : l - 16] = l < 32 ? xv : gv;
         }
       }
       const float gmk4 = gmk * A.ik4;
@@ -1624,7 +1626,7 @@ static XcdWeights xcd_weights_from_env() {
 }
 
 int sg_ntn_wgrad_run(const float *ntn, int64_t n_pairs, int D, int oW, int oV, int obn, int C,
-                     float *slab, int blocks, hipStream_t st);
+                     float *slab, int blocks, hipStream_t st, bool compact);
 
 // The host side of sg_fast_run.  The translation unit sg_fast_att.hip compiles this file
 // again with SG_FAST_ATT_TU defined and instantiates only the Attention kernels (the
@@ -1740,7 +1742,7 @@ static int fast_run_impl(const sg_model_t *m, const SgGenPlan &P, bool bwd, cons
 #endif
   if (avg && bwd) {   // the NTN W / V / bias gradients from the per-pair buffer
     const int rc = sg_ntn_wgrad_run(ntn, n_pairs, FH2, P.offW, P.offV, P.offB, P.n_params + 1,
-                                    slab, c.blocks, stream);
+                                    slab, c.blocks, stream, true);   // compact rows
     if (rc != SG_OK) return rc;
   }
   if (blocks_out) *blocks_out = c.blocks;

@@ -913,12 +913,18 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast32_kernel(F32Args A) {
 // global round trip per 64-pair chunk, 131 µs with D's tiles only, 70 µs double-buffered,
 // 62 µs at 8 waves (profiles/r06_e, r06_f).
 constexpr int WG_CHUNK = 64;   // pairs staged per LDS round
+// The pooled stacks' (D = 16) compact row: x1[16] | x2[16] | gm[10], zeros, and a 1 in the
+// last slot (x2's constant entry; x1's is the kernel's VALU column sum, !ROW1)
+constexpr int NBUF16 = 48;
+constexpr int NB16_ZERO = 46, NB16_ONE = 47;
 
-template <int NTW, bool ROW1, int NWV>
+template <int NTW, bool ROW1, int NWV, int NB>
 __global__ void __launch_bounds__(64 * NWV) sg_ntn_wgrad_kernel(const float *__restrict__ ntn,
                                                           int64_t n_pairs, int D, int oW,
                                                           int oV, int obn, int C,
                                                           float *__restrict__ slab) {
+  static_assert(NB == NBUF || (NB == NBUF16 && !ROW1), "row layouts");
+  constexpr int NBUF = NB;   // floats per pair row (the capacity-32 layout or the compact one)
   constexpr int CH = WG_CHUNK * NWV / 4, NT = 64 * NWV;   // pairs per chunk, threads
   __shared__ __attribute__((aligned(16))) float st[CH * NBUF];
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
@@ -933,8 +939,13 @@ __global__ void __launch_bounds__(64 * NWV) sg_ntn_wgrad_kernel(const float *__r
   for (int t = 0; t < NTW; ++t) {
     const int c = 16 * (w + NWV * t) + j;
     const int cc = c < DK ? c : 0;
-    cb_[t] = NC + cc / FK;          // x2[b'] offset in the pair's buffer row
-    ck_[t] = c < DK ? 2 * NC + cc % FK : 2 * NC + 15;   // gm[k] (slot 15 is 0: k < FK only)
+    if constexpr (NB == NBUF16) {   // (D = 16)
+      cb_[t] = cc / FK < 16 ? 16 + cc / FK : NB16_ONE;
+      ck_[t] = c < DK ? 32 + cc % FK : NB16_ZERO;
+    } else {
+      cb_[t] = NC + cc / FK;          // x2[b'] offset in the pair's buffer row
+      ck_[t] = c < DK ? 2 * NC + cc % FK : 2 * NC + 15;   // gm[k] (slot 15 is 0: k < FK only)
+    }
   }
   f4 acc[2][NTW];
   float csum[NTW];   // !ROW1: Σ of this lane's pairs' products, column 16 (w + 4t) + j
@@ -1062,21 +1073,26 @@ int64_t sg_fast32_slab_floats(const SgGenPlan &P, int64_t n_pairs) {
 
 int64_t sg_fast32_ntn_floats(int64_t n_pairs) { return n_pairs * NBUF; }
 
-// NTN W / V / bias gradients from a per-pair buffer [n_pairs][80] (x1|1, x2|1 at
-// capacity 32, gm at 64) into the NTN columns of slab rows 0..blocks-1 (also used by
-// sg_fast's Average stack, D = 16)
+// NTN W / V / bias gradients from a per-pair buffer into the NTN columns of slab rows
+// 0..blocks-1: rows [n_pairs][80] (x1|1, x2|1 at capacity 32, gm at 64) for sg_fast32,
+// or with `compact` (sg_fast's Average / Attention stacks, D = 16) the compact rows
+// [n_pairs][48] (x1 | x2 | gm, 0, 1: NBUF16): 192 instead of 320 bytes written and read per
+// pair
 int sg_ntn_wgrad_run(const float *ntn, int64_t n_pairs, int D, int oW, int oV, int obn, int C,
-                     float *slab, int blocks, hipStream_t st) {
-  if (D < 1 || D > 31 || obn < 0) return SG_ERR_ARG;
-  // column tiles per wave: ceil(ceil((D + 1) K / 16) / 4)
-  const int nct = ((D + 1) * FK + 15) / 16, ntw = (nct + 3) / 4;
-  // D <= 15: rows a <= D fit the first tile; D = 16 (the Average stack): row a = 16 on VALU
-  if (D <= 16 && nct <= 16)   // 8 waves of 2 tiles
-    hipLaunchKernelGGL((sg_ntn_wgrad_kernel<2, false, 8>), dim3(blocks), dim3(512), 0, st, ntn,
-                       n_pairs, D, oW, oV, obn, C, slab);
+                     float *slab, int blocks, hipStream_t st, bool compact) {
+  if (D < 1 || D > 31 || obn < 0 || (compact && D != 16)) return SG_ERR_ARG;
+  // column tiles: ceil((D + 1) K / 16)
+  const int nct = ((D + 1) * FK + 15) / 16;
+  // D <= 15: rows a <= D fit the first tile; D = 16: row a = 16 on VALU
+  if (compact)   // 8 waves of 2 tiles, compact rows
+    hipLaunchKernelGGL((sg_ntn_wgrad_kernel<2, false, 8, NBUF16>), dim3(blocks), dim3(512), 0,
+                       st, ntn, n_pairs, D, oW, oV, obn, C, slab);
+  else if (D <= 16 && nct <= 16)
+    hipLaunchKernelGGL((sg_ntn_wgrad_kernel<2, false, 8, NBUF>), dim3(blocks), dim3(512), 0, st,
+                       ntn, n_pairs, D, oW, oV, obn, C, slab);
   else
-    hipLaunchKernelGGL((sg_ntn_wgrad_kernel<5, true, 4>), dim3(blocks), dim3(256), 0, st, ntn,
-                       n_pairs, D, oW, oV, obn, C, slab);
+    hipLaunchKernelGGL((sg_ntn_wgrad_kernel<5, true, 4, NBUF>), dim3(blocks), dim3(256), 0, st,
+                       ntn, n_pairs, D, oW, oV, obn, C, slab);
   return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_HIP;
 }
 
@@ -1168,7 +1184,7 @@ int sg_fast32_run(const sg_model_t *m, const SgGenPlan &P, bool bwd, const void 
 #undef SG32_LAUNCH
   if (bwd) {
     const int rc = sg_ntn_wgrad_run((const float *)ntn, n_pairs, P.D, P.offW, P.offV, P.offB,
-                                    P.n_params + 1, slab, c.blocks, stream);
+                                    P.n_params + 1, slab, c.blocks, stream, false);
     if (rc != SG_OK) return rc;
   }
   if (blocks_out) *blocks_out = c.blocks;
