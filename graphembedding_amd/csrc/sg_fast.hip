@@ -544,21 +544,64 @@ __global__ void __launch_bounds__(64 * MAXW) sg_fast_kernel(FastArgs A) {
       A.ad_out[3] = (float)((double)A.ad_wd * 0.5 * ss);
     }
   }
-  for (int i = tid; i < (d_in + 1) * FH1; i += blockDim.x)
-    sW0[i] = i < d_in * FH1 ? stg[A.oW0 + i] * (A.ik0 * A.ik1) : 0.f;
-  for (int i = tid; i < DN * FK * WR; i += blockDim.x) {
+  // the tables' elements of this thread: (a) the sources of every table read from the staged
+  // copy, then (b) all stores (512-thread blocks, the launch's shape).  Strided loops that
+  // read and store in turn took one LDS round trip per element (the compiler may not move
+  // a read above a store to the same array): ≈20 round trips of the 1.8 µs table build.
+  auto wa_src = [&](int i, bool tr) -> float {   // sWa (tr: sWb) element i
     const int x = i / (FK * WR), rem = i - x * FK * WR, k = rem / WR, y = rem - k * WR;
-    sWa[i] = y < DN ? stg[A.oW + (x * DN + y) * FK + k] : 0.f;
-    sWb[i] = y < DN ? stg[A.oW + (y * DN + x) * FK + k] : 0.f;
-  }
-  for (int i = tid; i < FK * VS; i += blockDim.x) {
+    return y < DN ? stg[A.oW + (tr ? (y * DN + x) : (x * DN + y)) * FK + k] : 0.f;
+  };
+  auto v_src = [&](int i) -> float {
     const int k = i / VS, c = i - k * VS;
-    sV[i] = c < 2 * DN ? stg[A.oV + k * 2 * DN + c] : 0.f;
-  }
-  for (int i = tid; i < FH1 * FH2; i += blockDim.x) {
-    const float w = stg[A.oW1 + i];
-    sW1[(i / FH2) * W1S + i % FH2] = w * A.ik1;
-    sW1T[(i % FH2) * W1TS + i / FH2] = w;
+    return c < 2 * DN ? stg[A.oV + k * 2 * DN + c] : 0.f;
+  };
+  constexpr int NWA = DN * FK * WR, KWA = (NWA + 511) / 512, NVT = FK * VS, KV = (NVT + 511) / 512;
+  static_assert(FH1 * FH2 == 512, "one W1 element per thread of a 512-thread block");
+  const int nw0 = (d_in + 1) * FH1;
+  if (bdx == 512 && nw0 <= 3 * 512) {
+    float r0[3], ra[KWA], rb[KWA], rv[KV];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int i = min(tid + 512 * k, nw0 - 1);
+      r0[k] = i < d_in * FH1 ? stg[A.oW0 + i] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < KWA; ++k) {
+      const int i = min(tid + 512 * k, NWA - 1);
+      ra[k] = wa_src(i, false);
+      rb[k] = wa_src(i, true);
+    }
+#pragma unroll
+    for (int k = 0; k < KV; ++k) rv[k] = v_src(min(tid + 512 * k, NVT - 1));
+    const float w1 = stg[A.oW1 + tid];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      if (tid + 512 * k < nw0) sW0[tid + 512 * k] = r0[k] * (A.ik0 * A.ik1);
+#pragma unroll
+    for (int k = 0; k < KWA; ++k)
+      if (tid + 512 * k < NWA) {
+        sWa[tid + 512 * k] = ra[k];
+        sWb[tid + 512 * k] = rb[k];
+      }
+#pragma unroll
+    for (int k = 0; k < KV; ++k)
+      if (tid + 512 * k < NVT) sV[tid + 512 * k] = rv[k];
+    sW1[(tid / FH2) * W1S + tid % FH2] = w1 * A.ik1;
+    sW1T[(tid % FH2) * W1TS + tid / FH2] = w1;
+  } else {   // smaller blocks (batches of a few pairs)
+    for (int i = tid; i < nw0; i += bdx)
+      sW0[i] = i < d_in * FH1 ? stg[A.oW0 + i] * (A.ik0 * A.ik1) : 0.f;
+    for (int i = tid; i < NWA; i += bdx) {
+      sWa[i] = wa_src(i, false);
+      sWb[i] = wa_src(i, true);
+    }
+    for (int i = tid; i < NVT; i += bdx) sV[i] = v_src(i);
+    for (int i = tid; i < FH1 * FH2; i += bdx) {
+      const float w = stg[A.oW1 + i];
+      sW1[(i / FH2) * W1S + i % FH2] = w * A.ik1;
+      sW1T[(i % FH2) * W1TS + i / FH2] = w;
+    }
   }
   for (int i = tid; i < 2 * 3 * 64; i += blockDim.x) {
     const int t = i / 192, term = (i / 64) % 3, ln = i & 63;
